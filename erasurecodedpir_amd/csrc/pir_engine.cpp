@@ -1,0 +1,529 @@
+// pir_engine.cpp -- host side of the C ABI in include/pir_engine.h.
+//
+// One engine = one GPU holding one shard (or one 2^-G partition of a logical shard) in HBM,
+// laid out as rows of `pitch` = round_up(record_bytes, 16) bytes (zero padding), so every
+// lane of the scan reads aligned 16-byte chunks.  An answer is four kernels on one stream:
+//   key prep -> tree (frontier + leaves) -> GF(2^8) scan -> slab reduce
+// plus, for a split shard, an RCCL all-gather of the per-partition answers and an XOR fold
+// (RCCL has no XOR reduction op).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/pir_engine.h"
+#include "pir_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess)                                                                   \
+      return fail(PIR_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, \
+                  __LINE__);                                                                \
+  } while (0)
+
+#define RCCL_TRY(expr)                                                                        \
+  do {                                                                                        \
+    ncclResult_t _r = (expr);                                                                 \
+    if (_r != ncclSuccess) return fail(PIR_ECOMM, "%s failed: %s", #expr, ncclGetErrorString(_r)); \
+  } while (0)
+
+int ilog2_exact(uint64_t v) {
+  if (v == 0 || (v & (v - 1))) return -1;
+  int l = 0;
+  while ((1ull << l) < v) ++l;
+  return l;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace
+
+struct pir_engine {
+  pir_engine_config cfg{};
+  int nrp = 1;
+  uint32_t pitch = 0;
+  uint64_t rows = 0;  // rows held = 2^(n - G)
+  int key_len = 0;
+  int num_cus = 256;
+  hipStream_t stream = nullptr;
+  uint8_t* d_shard = nullptr;
+  uint8_t* d_key_raw = nullptr;  // max_batch keys
+  pir::DevKey* d_keys = nullptr; // max_batch parsed keys
+  int max_batch = 0;
+  uint4* d_front_s = nullptr;
+  uint32_t* d_front_t = nullptr;
+  uint8_t* d_c = nullptr;
+  uint8_t* d_slabs = nullptr;
+  size_t slab_cap = 0;
+  uint8_t* d_part = nullptr;    // nq*efs partition answer
+  uint8_t* d_gather = nullptr;  // nranks*nq*efs
+  uint8_t* d_result = nullptr;  // nq*efs (host-API staging)
+  uint8_t* h_key = nullptr;     // pinned
+  uint8_t* h_res = nullptr;     // pinned
+  std::vector<DevBuf> user;     // pir_engine_alloc_dev
+  std::mutex mu;
+  uint64_t byz_counter = 0;
+  // profiling: a ring of event sets, one per answer, read back after a sync
+  struct ProfSlot {
+    hipEvent_t ev[7];
+  };
+  std::vector<ProfSlot> prof;
+  int prof_next = 0, prof_count = 0;
+  hipEvent_t* ev = nullptr;  // the current answer's slot (nullptr: profiling off)
+  // RCCL
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+namespace {
+
+int ensure_batch(pir_engine* e, int nk) {
+  if (nk <= e->max_batch) return PIR_OK;
+  if (e->d_key_raw) (void)hipFree(e->d_key_raw);
+  if (e->d_keys) (void)hipFree(e->d_keys);
+  e->d_key_raw = nullptr;
+  e->d_keys = nullptr;
+  HIP_TRY(hipMalloc(&e->d_key_raw, (size_t)nk * e->key_len));
+  HIP_TRY(hipMalloc(&e->d_keys, (size_t)nk * sizeof(pir::DevKey)));
+  e->max_batch = nk;
+  return PIR_OK;
+}
+
+int ensure_slabs(pir_engine* e, size_t bytes) {
+  if (bytes <= e->slab_cap) return PIR_OK;
+  if (e->d_slabs) (void)hipFree(e->d_slabs);
+  e->d_slabs = nullptr;
+  HIP_TRY(hipMalloc(&e->d_slabs, bytes));
+  e->slab_cap = bytes;
+  return PIR_OK;
+}
+
+// Answer one partition slice: rows [row0, row0 + 2^(n - log_parts_total)) of this engine
+// with the tree rooted at `prefix` (depth log_parts_total).  d_key points at ONE parsed key.
+int answer_core(pir_engine* e, const pir::DevKey* d_key, int log_parts_total, uint64_t prefix,
+                uint64_t row0, uint8_t* d_out, hipStream_t s) {
+  const auto& c = e->cfg;
+  const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix);
+  const uint64_t nrec = pl.nleaves;
+  const pir::ScanShape sh = pir::make_scan_shape(nrec, e->pitch, c.num_rounds, e->num_cus);
+  int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
+  if (rc) return rc;
+  hipEvent_t* ev = e->ev;
+  if (ev) HIP_TRY(hipEventRecord(ev[1], s));
+  HIP_TRY(pir::launch_tree(pl, d_key, e->d_front_s, e->d_front_t, e->d_c, e->nrp, s,
+                           ev ? ev[2] : nullptr));
+  if (ev) HIP_TRY(hipEventRecord(ev[3], s));
+  HIP_TRY(pir::launch_scan(sh, e->d_shard + row0 * e->pitch, nrec, e->d_c, e->d_slabs, s));
+  if (ev) HIP_TRY(hipEventRecord(ev[4], s));
+  HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, d_out, s));
+  if (ev) HIP_TRY(hipEventRecord(ev[5], s));
+  return PIR_OK;
+}
+
+int check_key_ptr(const void* p) { return p ? PIR_OK : fail(PIR_EINVAL, "null key"); }
+
+const char* const kPhaseNames[6] = {"key_prep", "tree_frontier", "tree_leaves",
+                                    "scan", "reduce", "comm_fold"};
+
+// Average per-phase times over the answers recorded since the last read.
+int read_timings(pir_engine* e, pir_kernel_time* out, int max) {
+  const int n = std::min(max, 6);
+  if (e->prof.empty() || e->prof_count == 0) return 0;
+  const int cnt = e->prof_count, sz = (int)e->prof.size();
+  HIP_TRY(hipEventSynchronize(e->prof[(e->prof_next + sz - 1) % sz].ev[6]));
+  for (int i = 0; i < n; ++i) {
+    double acc = 0;
+    for (int k = 0; k < cnt; ++k) {
+      const auto& sl = e->prof[(e->prof_next + sz - cnt + k) % sz];
+      float ms = 0;
+      HIP_TRY(hipEventElapsedTime(&ms, sl.ev[i], sl.ev[i + 1]));
+      acc += ms;
+    }
+    snprintf(out[i].name, sizeof out[i].name, "%s", kPhaseNames[i]);
+    out[i].ms = (float)(acc / cnt);
+  }
+  e->prof_count = 0;
+  return n;
+}
+
+int answer_dev_locked(pir_engine* e, const uint8_t* d_key, uint8_t* d_result, hipStream_t s) {
+  const auto& c = e->cfg;
+  const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
+  e->ev = nullptr;
+  if (!e->prof.empty()) {
+    e->ev = e->prof[e->prof_next].ev;
+    e->prof_next = (e->prof_next + 1) % (int)e->prof.size();
+    e->prof_count = std::min(e->prof_count + 1, (int)e->prof.size());
+  }
+  hipEvent_t* ev = e->ev;
+  if (ev) HIP_TRY(hipEventRecord(ev[0], s));
+  if (c.is_byzantine) {  // server.cpp:116-119: random answer bytes
+    HIP_TRY(pir::launch_fill_random(d_result, out_bytes, 0xB42u + (++e->byz_counter), s));
+    if (ev)
+      for (int i = 1; i < 7; ++i) HIP_TRY(hipEventRecord(ev[i], s));
+    return PIR_OK;
+  }
+  HIP_TRY(pir::launch_key_prep(d_key, e->key_len, 1, c.num_parties, c.log_num_records,
+                               c.num_rounds, c.party_index - 1, e->d_keys, s));
+  uint8_t* part_out = e->comm ? e->d_part : d_result;
+  int rc = answer_core(e, e->d_keys, c.log_num_partitions, (uint64_t)c.partition_index, 0,
+                       part_out, s);
+  if (rc) return rc;
+  if (e->comm) {
+    RCCL_TRY(ncclAllGather(e->d_part, e->d_gather, out_bytes, ncclUint8, e->comm, s));
+    HIP_TRY(pir::launch_xor_fold(e->d_gather, e->nranks, out_bytes, d_result, s));
+  }
+  if (ev) HIP_TRY(hipEventRecord(ev[6], s));
+  e->ev = nullptr;
+  return PIR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pir_engine_last_error(void) { return g_err.c_str(); }
+
+int pir_engine_key_len(int p, int n, int nq) {  // utils.cpp:85-90
+  return 16 + n * (p - 1) * (16 + 2 * p - 2) + nq * (p - 1);
+}
+
+int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
+  if (!cfg || !out) return fail(PIR_EINVAL, "null argument");
+  const auto& c = *cfg;
+  if (c.num_parties < 2 || c.num_parties > PIR_MAX_PARTIES)
+    return fail(PIR_EINVAL, "num_parties %d outside [2,%d]", c.num_parties, PIR_MAX_PARTIES);
+  if (c.party_index < 1 || c.party_index > c.num_parties)
+    return fail(PIR_EINVAL, "party_index %d outside [1,%d]", c.party_index, c.num_parties);
+  if (c.num_rounds < 1 || c.num_rounds > PIR_MAX_ROUNDS)
+    return fail(PIR_EINVAL, "num_rounds %d outside [1,%d]", c.num_rounds, PIR_MAX_ROUNDS);
+  if (c.log_num_records < 0 || c.log_num_records > PIR_MAX_LOG_RECORDS)
+    return fail(PIR_EINVAL, "log_num_records %d", c.log_num_records);
+  if (c.record_bytes < 1) return fail(PIR_EINVAL, "record_bytes must be >= 1");
+  if (c.log_num_partitions < 0 || c.log_num_partitions > c.log_num_records ||
+      c.partition_index < 0 || (uint64_t)c.partition_index >= (1ull << c.log_num_partitions))
+    return fail(PIR_EINVAL, "bad partition %d of 2^%d", c.partition_index, c.log_num_partitions);
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (c.device < 0 || c.device >= ndev) return fail(PIR_EINVAL, "device %d of %d", c.device, ndev);
+  HIP_TRY(hipSetDevice(c.device));
+
+  auto* e = new pir_engine;
+  e->cfg = c;
+  e->nrp = c.num_rounds == 1 ? 1 : (c.num_rounds == 2 ? 2 : (c.num_rounds <= 4 ? 4 : (c.num_rounds <= 8 ? 8 : 16)));
+  e->pitch = (c.record_bytes + 15u) & ~15u;
+  e->rows = 1ull << (c.log_num_records - c.log_num_partitions);
+  e->key_len = pir_engine_key_len(c.num_parties, c.log_num_records, c.num_rounds);
+  auto cleanup = [&](int rc) { pir_engine_destroy(e); return rc; };
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, c.device) == hipSuccess) e->num_cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(PIR_EHIP, "hipStreamCreate failed"));
+  pir::upload_aes_table(e->stream);
+  const size_t shard_bytes = (size_t)e->rows * e->pitch;
+  if (hipMalloc(&e->d_shard, shard_bytes) != hipSuccess)
+    return cleanup(fail(PIR_ENOMEM, "hipMalloc shard %zu bytes", shard_bytes));
+  if (hipMemsetAsync(e->d_shard, 0, shard_bytes, e->stream) != hipSuccess)
+    return cleanup(fail(PIR_EHIP, "hipMemset shard"));
+  const pir::TreePlan pl = pir::make_plan(c.log_num_records, c.log_num_partitions, 0);
+  const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
+  if (hipMalloc(&e->d_front_s, pl.nfront * sizeof(uint4)) != hipSuccess ||
+      hipMalloc(&e->d_front_t, pl.nfront * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&e->d_c, (size_t)e->rows * e->nrp) != hipSuccess ||
+      hipMalloc(&e->d_part, out_bytes) != hipSuccess ||
+      hipMalloc(&e->d_result, out_bytes) != hipSuccess ||
+      hipHostMalloc(&e->h_key, e->key_len) != hipSuccess ||
+      hipHostMalloc(&e->h_res, out_bytes) != hipSuccess)
+    return cleanup(fail(PIR_ENOMEM, "workspace allocation failed"));
+  int rc = ensure_batch(e, 1);
+  if (rc) return cleanup(rc);
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return cleanup(fail(PIR_EHIP, "sync"));
+  *out = e;
+  return PIR_OK;
+}
+
+void pir_engine_destroy(pir_engine_t* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->cfg.device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->comm) (void)ncclCommDestroy(e->comm);
+  for (auto* p : {(void*)e->d_shard, (void*)e->d_key_raw, (void*)e->d_keys, (void*)e->d_front_s,
+                  (void*)e->d_front_t, (void*)e->d_c, (void*)e->d_slabs, (void*)e->d_part,
+                  (void*)e->d_gather, (void*)e->d_result})
+    if (p) (void)hipFree(p);
+  for (auto& b : e->user) (void)hipFree(b.p);
+  if (e->h_key) (void)hipHostFree(e->h_key);
+  if (e->h_res) (void)hipHostFree(e->h_res);
+  for (auto& sl : e->prof)
+    for (auto& ev : sl.ev) (void)hipEventDestroy(ev);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+uint64_t pir_engine_num_rows(const pir_engine_t* e) { return e ? e->rows : 0; }
+
+int pir_engine_set_shard(pir_engine_t* e, const uint8_t* host, uint64_t row0, uint64_t nrows,
+                         uint64_t src_pitch) {
+  if (!e || (!host && nrows)) return fail(PIR_EINVAL, "null argument");
+  if (row0 + nrows > e->rows) return fail(PIR_EINVAL, "rows [%llu,%llu) beyond %llu",
+                                          (unsigned long long)row0,
+                                          (unsigned long long)(row0 + nrows),
+                                          (unsigned long long)e->rows);
+  if (src_pitch < e->cfg.record_bytes) return fail(PIR_EINVAL, "src_pitch < record_bytes");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  // 2-D copy writes record_bytes per row; the pad bytes stay zero from the create memset
+  HIP_TRY(hipMemcpy2DAsync(e->d_shard + row0 * e->pitch, e->pitch, host, src_pitch,
+                           e->cfg.record_bytes, nrows, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return PIR_OK;
+}
+
+int pir_engine_set_shard_rows(pir_engine_t* e, const uint8_t* const* rows, uint64_t row0,
+                              uint64_t nrows) {
+  if (!e || (!rows && nrows)) return fail(PIR_EINVAL, "null argument");
+  if (row0 + nrows > e->rows) return fail(PIR_EINVAL, "rows beyond shard");
+  const uint32_t efs = e->cfg.record_bytes;
+  const uint64_t chunk_rows = std::max<uint64_t>(1, (64ull << 20) / efs);
+  std::vector<uint8_t> stage((size_t)std::min(chunk_rows, nrows) * efs);
+  for (uint64_t r = 0; r < nrows; r += chunk_rows) {
+    const uint64_t m = std::min(chunk_rows, nrows - r);
+    for (uint64_t i = 0; i < m; ++i) memcpy(stage.data() + i * efs, rows[r + i], efs);
+    int rc = pir_engine_set_shard(e, stage.data(), row0 + r, m, efs);
+    if (rc) return rc;
+  }
+  return PIR_OK;
+}
+
+int pir_engine_fill_shard_random(pir_engine_t* e, uint64_t seed) {
+  if (!e) return fail(PIR_EINVAL, "null engine");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const uint64_t row0 = (uint64_t)e->cfg.partition_index * e->rows;
+  HIP_TRY(pir::launch_fill_shard(e->d_shard, e->rows, e->pitch, e->cfg.record_bytes, row0, seed,
+                                 e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return PIR_OK;
+}
+
+int pir_engine_get_shard_row(pir_engine_t* e, uint64_t row, uint8_t* out) {
+  if (!e || !out) return fail(PIR_EINVAL, "null argument");
+  if (row >= e->rows) return fail(PIR_EINVAL, "row %llu beyond shard", (unsigned long long)row);
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipMemcpyAsync(out, e->d_shard + row * e->pitch, e->cfg.record_bytes,
+                         hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return PIR_OK;
+}
+
+int pir_engine_answer_dev(pir_engine_t* e, const uint8_t* d_key, uint8_t* d_result,
+                          void* stream) {
+  if (!e || !d_result) return fail(PIR_EINVAL, "null argument");
+  if (int rc = check_key_ptr(d_key)) return rc;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  return answer_dev_locked(e, d_key, d_result, s);
+}
+
+int pir_engine_answer_batch_dev(pir_engine_t* e, const uint8_t* d_keys, int num_keys,
+                                uint8_t* d_result, void* stream) {
+  if (!e || !d_result || num_keys < 0) return fail(PIR_EINVAL, "bad argument");
+  if (int rc = check_key_ptr(d_keys)) return rc;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  const size_t out_bytes = (size_t)e->cfg.num_rounds * e->cfg.record_bytes;
+  for (int q = 0; q < num_keys; ++q) {
+    int rc = answer_dev_locked(e, d_keys + (size_t)q * e->key_len, d_result + q * out_bytes, s);
+    if (rc) return rc;
+  }
+  return PIR_OK;
+}
+
+int pir_engine_answer(pir_engine_t* e, const uint8_t* key, uint8_t* result) {
+  if (!e || !result) return fail(PIR_EINVAL, "null argument");
+  if (int rc = check_key_ptr(key)) return rc;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const size_t out_bytes = (size_t)e->cfg.num_rounds * e->cfg.record_bytes;
+  memcpy(e->h_key, key, e->key_len);
+  HIP_TRY(hipMemcpyAsync(e->d_key_raw, e->h_key, e->key_len, hipMemcpyHostToDevice, e->stream));
+  int rc = answer_dev_locked(e, e->d_key_raw, e->d_result, e->stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(e->h_res, e->d_result, out_bytes, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memcpy(result, e->h_res, out_bytes);
+  return PIR_OK;
+}
+
+int pir_engine_answer_slice(pir_engine_t* e, const uint8_t* key, int thread_num, int num_threads,
+                            uint8_t* result) {
+  if (!e || !result) return fail(PIR_EINVAL, "null argument");
+  if (int rc = check_key_ptr(key)) return rc;
+  const int lt = ilog2_exact((uint64_t)num_threads);
+  const auto& c = e->cfg;
+  if (lt < 0 || c.log_num_partitions + lt > c.log_num_records)
+    return fail(PIR_EINVAL, "num_threads %d must be a power of two <= 2^%d", num_threads,
+                c.log_num_records - c.log_num_partitions);
+  if (thread_num < 0 || thread_num >= num_threads)
+    return fail(PIR_EINVAL, "thread_num %d of %d", thread_num, num_threads);
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(c.device));
+  const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
+  // NB: the reference's Thread variant computes the honest answer even when isByzantine is
+  // set (both branches of server.cpp:526-541 are identical); mirrored here.
+  memcpy(e->h_key, key, e->key_len);
+  HIP_TRY(hipMemcpyAsync(e->d_key_raw, e->h_key, e->key_len, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(pir::launch_key_prep(e->d_key_raw, e->key_len, 1, c.num_parties, c.log_num_records,
+                               c.num_rounds, c.party_index - 1, e->d_keys, e->stream));
+  const uint64_t prefix = ((uint64_t)c.partition_index << lt) | (uint64_t)thread_num;
+  const uint64_t row0 = (uint64_t)thread_num * (e->rows >> lt);
+  int rc = answer_core(e, e->d_keys, c.log_num_partitions + lt, prefix, row0, e->d_result,
+                       e->stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(e->h_res, e->d_result, out_bytes, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memcpy(result, e->h_res, out_bytes);
+  return PIR_OK;
+}
+
+int pir_engine_eval_all(pir_engine_t* e, const uint8_t* key, uint8_t* out) {
+  if (!e || !out) return fail(PIR_EINVAL, "null argument");
+  if (int rc = check_key_ptr(key)) return rc;
+  std::lock_guard<std::mutex> lk(e->mu);
+  const auto& c = e->cfg;
+  HIP_TRY(hipSetDevice(c.device));
+  memcpy(e->h_key, key, e->key_len);
+  HIP_TRY(hipMemcpyAsync(e->d_key_raw, e->h_key, e->key_len, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(pir::launch_key_prep(e->d_key_raw, e->key_len, 1, c.num_parties, c.log_num_records,
+                               c.num_rounds, c.party_index - 1, e->d_keys, e->stream));
+  const pir::TreePlan pl =
+      pir::make_plan(c.log_num_records, c.log_num_partitions, (uint64_t)c.partition_index);
+  HIP_TRY(pir::launch_tree(pl, e->d_keys, e->d_front_s, e->d_front_t, e->d_c, e->nrp, e->stream));
+  std::vector<uint8_t> ct((size_t)e->rows * e->nrp);
+  HIP_TRY(hipMemcpyAsync(ct.data(), e->d_c, ct.size(), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (uint64_t i = 0; i < e->rows; ++i)
+    for (int a = 0; a < c.num_rounds; ++a) out[(size_t)a * e->rows + i] = ct[i * e->nrp + a];
+  return PIR_OK;
+}
+
+void* pir_engine_stream(pir_engine_t* e) { return e ? (void*)e->stream : nullptr; }
+
+int pir_engine_sync(pir_engine_t* e) {
+  if (!e) return fail(PIR_EINVAL, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return PIR_OK;
+}
+
+int pir_engine_alloc_dev(pir_engine_t* e, size_t bytes, void** d_ptr) {
+  if (!e || !d_ptr) return fail(PIR_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  void* p = nullptr;
+  HIP_TRY(hipMalloc(&p, bytes ? bytes : 1));
+  e->user.push_back({p, bytes});
+  *d_ptr = p;
+  return PIR_OK;
+}
+
+int pir_engine_memcpy_h2d(pir_engine_t* e, void* d_dst, const void* h_src, size_t bytes) {
+  if (!e) return fail(PIR_EINVAL, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return PIR_OK;
+}
+
+int pir_engine_memcpy_d2h(pir_engine_t* e, void* h_dst, const void* d_src, size_t bytes) {
+  if (!e) return fail(PIR_EINVAL, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return PIR_OK;
+}
+
+int pir_engine_set_profiling(pir_engine_t* e, int slots) {
+  if (!e || slots < 0) return fail(PIR_EINVAL, "bad argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (auto& sl : e->prof)
+    for (auto& ev : sl.ev) (void)hipEventDestroy(ev);
+  e->prof.assign((size_t)slots, {});
+  e->prof_next = e->prof_count = 0;
+  for (auto& sl : e->prof)
+    for (auto& ev : sl.ev) HIP_TRY(hipEventCreate(&ev));
+  return PIR_OK;
+}
+
+int pir_engine_last_timings(pir_engine_t* e, pir_kernel_time* out, int max) {
+  if (!e || !out) return fail(PIR_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  return read_timings(e, out, max);
+}
+
+int pir_engine_get_shard(pir_engine_t* e, uint64_t row0, uint64_t nrows, uint8_t* out) {
+  if (!e || (!out && nrows)) return fail(PIR_EINVAL, "null argument");
+  if (row0 + nrows > e->rows) return fail(PIR_EINVAL, "rows beyond shard");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipMemcpy2DAsync(out, e->cfg.record_bytes, e->d_shard + row0 * e->pitch, e->pitch,
+                           e->cfg.record_bytes, nrows, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return PIR_OK;
+}
+
+int pir_comm_unique_id(uint8_t id[PIR_COMM_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) == PIR_COMM_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId u;
+  RCCL_TRY(ncclGetUniqueId(&u));
+  memcpy(id, &u, sizeof u);
+  return PIR_OK;
+}
+
+int pir_comm_attach(pir_engine_t* e, const uint8_t id[PIR_COMM_ID_BYTES], int nranks, int rank) {
+  if (!e || !id) return fail(PIR_EINVAL, "null argument");
+  if (nranks != (1 << e->cfg.log_num_partitions) || rank != e->cfg.partition_index)
+    return fail(PIR_EINVAL, "rank %d/%d does not match partition %d of 2^%d", rank, nranks,
+                e->cfg.partition_index, e->cfg.log_num_partitions);
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  RCCL_TRY(ncclCommInitRank(&e->comm, nranks, u, rank));
+  e->nranks = nranks;
+  e->rank = rank;
+  HIP_TRY(hipMalloc(&e->d_gather, (size_t)nranks * e->cfg.num_rounds * e->cfg.record_bytes));
+  return PIR_OK;
+}
+
+}  // extern "C"

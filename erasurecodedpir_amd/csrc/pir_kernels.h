@@ -1,0 +1,70 @@
+// pir_kernels.h -- internal interface between the HIP kernels (pir_kernels.hip) and the
+// engine host code (pir_engine.cpp).  Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pir {
+
+constexpr int kMaxLevels = 40;  // PIR_MAX_LOG_RECORDS
+constexpr int kMaxCW = 16;      // p - 1 <= 16
+constexpr int kNodeCap = 1024;  // tree nodes per LDS level buffer
+constexpr int kTreeThreads = 512;
+constexpr int kScanThreads = 256;
+constexpr int kColGroupLanes = 64;  // one wave's lanes cover a column group of a record
+
+// One DPF key, parsed for the device (written by k_key_prep from the raw key bytes whose
+// layout is genOptimizedDPF's: dpf_tree.cpp:254-269).
+struct DevKey {
+  uint4 root_seed;               // key[0:16]
+  uint32_t root_t;               // party control bits: bit (party0-1) (dpf_tree.cpp:496-502)
+  uint32_t p, n, nq;
+  uint4 scw[kMaxLevels * kMaxCW];      // sCW[L][j]
+  uint32_t tcw[kMaxLevels * kMaxCW];   // tCW[L][j] packed: bit k = key byte (16+k) of the CW
+  uint4 lastcw[kMaxCW];                // lastCW[j][a] as byte a (a < nq; zero above)
+};
+
+// Key-independent shape of one answer pass (one partition of the logical tree).
+struct TreePlan {
+  int n;            // full tree depth (LOG_NUM_ENCODED_FILES)
+  int log_parts;    // partition prefix depth
+  uint64_t prefix;  // partition index (path bits MSB first)
+  int g;            // frontier kernel: 2^g workgroups, each descends g more levels
+  int e;            // ... then expands e levels (frontier level F = log_parts + g + e)
+  int d;            // leaves kernel: expands d levels below the frontier
+  int tile;         // frontier nodes per leaves-kernel workgroup
+  uint64_t nfront;  // 2^(g+e)
+  uint64_t nleaves; // 2^(n - log_parts)
+};
+
+TreePlan make_plan(int n, int log_parts, uint64_t prefix);
+
+void upload_aes_table(hipStream_t s);  // Te0 (computed on the host) -> __constant__ memory
+
+hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys, int p, int n,
+                           int nq, int party0, DevKey* d_keys, hipStream_t s);
+hipError_t launch_tree(const TreePlan& pl, const DevKey* d_key, uint4* d_front_s,
+                       uint32_t* d_front_t, uint8_t* d_c, int nrp, hipStream_t s,
+                       hipEvent_t mid = nullptr);
+// scan rows [0, nrec) of `shard` (row pitch `pitch`) with coefficients cT[i*nrp + a]
+struct ScanShape {
+  int nq, nrp, vec;      // vec = dwords per lane chunk (4, 2, 1)
+  bool uniform;          // a record spans >= one wave (one record per wave row)
+  uint32_t pitch, cpr;   // bytes per row, chunks per row
+  uint32_t slab_bytes;   // per-workgroup partial = nq * 64 * vec * 4
+  dim3 grid;
+};
+ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus);
+hipError_t launch_scan(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
+                       const uint8_t* d_c, uint8_t* d_slabs, hipStream_t s);
+// XOR the slabs, compact pitch -> record_bytes: d_out[a*efs + b]
+hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t efs,
+                         uint8_t* d_out, hipStream_t s);
+// d_out[i] = XOR_r d_in[r*len + i]
+hipError_t launch_xor_fold(const uint8_t* d_in, int nranks, size_t len, uint8_t* d_out,
+                           hipStream_t s);
+hipError_t launch_fill_random(uint8_t* d, size_t bytes, uint64_t seed, hipStream_t s);
+hipError_t launch_fill_shard(uint8_t* d_shard, uint64_t rows, uint32_t pitch, uint32_t efs,
+                             uint64_t global_row0, uint64_t seed, hipStream_t s);
+
+}  // namespace pir

@@ -1,0 +1,594 @@
+// pir_kernels.hip -- CDNA4 (gfx950) kernels of the tree-DPF PIR answer path.
+//
+//   k_key_prep      raw genOptimizedDPF key bytes -> DevKey           (dpf_tree.cpp:504-519)
+//   k_tree_frontier root (or partition prefix) -> frontier level F    (dpf_tree.cpp:525-559)
+//   k_tree_leaves   frontier -> leaves -> DPF shares c[i][a]          (dpf_tree.cpp:525-580)
+//   k_scan          ans[a] ^= c[i][a] * shard[i]  over GF(2^8)        (server.cpp:121-127)
+//   k_reduce        XOR of per-workgroup partial answers              (server.cpp:553-562)
+//
+// AES-128 (the PRG G of utils.cpp:37-51 re-keys on every node seed) is a T-table cipher:
+// one 1 KiB table Te0 replicated 32x in LDS ([entry][lane & 31]) so every lane of a
+// 32-lane ds_read_b32 group hits its own bank; Te1..Te3 are byte rotations of Te0.
+// The GF(2^8) scan keeps, per lane, 8 bit-plane accumulators Z_k (Z_k ^= x when bit k of the
+// record's coefficient is set) and folds ans = sum_k alpha^k Z_k once at the end, so the
+// HBM stream costs ~1 VALU op per byte.
+#include "pir_kernels.h"
+#include "pir_aes.h"
+
+#include <algorithm>
+
+namespace pir {
+
+void upload_aes_table(hipStream_t s) { upload_te0(s); }
+
+// One third of a node expansion (dpf_tree.cpp:530-551).  role 0 / 1: the corrected left /
+// right child seed; role 2: packed child control bits (bits [0,p-1) left, [p-1,2p-2) right).
+__device__ __forceinline__ uint4 expand_role(const Te& T, const DevKey* __restrict__ K, int L,
+                                            uint4 seed, uint32_t t, int role, uint32_t pm1,
+                                            uint32_t tb_mask) {
+  uint4 o = aes_ctr_block(T, seed, (uint32_t)role);
+  uint4 cs = make_uint4(0, 0, 0, 0);
+  uint32_t ct = 0;
+  for (uint32_t j = 0; j < pm1; ++j) {  // parse_prg_output t bits + CW (dpf_tree.cpp:533-541)
+    uint32_t m = 0u - ((t >> j) & 1u);
+    cs = xor4(cs, and4(K->scw[L * kMaxCW + j], m));
+    ct ^= K->tcw[L * kMaxCW + j] & m;
+  }
+  if (role < 2) return xor4(o, cs);
+  o.x = (o.x & tb_mask) ^ ct;
+  return o;
+}
+
+struct TreeSmem {
+  uint32_t te[256 * 32];
+  uint4 s[2][kNodeCap];
+  uint32_t t[2][kNodeCap];
+};
+
+// One level of expansions inside a workgroup: parents in[off, off+W) -> children.
+// Children go to LDS buffer `out` (to_global == false) or to the global frontier arrays.
+__device__ __forceinline__ void expand_level(const Te& T, const DevKey* __restrict__ K, int L,
+                                             const uint4* in_s, const uint32_t* in_t, int off,
+                                             int W, uint4* out_s, uint32_t* out_t, uint32_t pm1,
+                                             uint32_t tb_mask) {
+  const uint32_t tmask = (1u << pm1) - 1u;
+  for (int task = threadIdx.x; task < 3 * W; task += blockDim.x) {
+    const int u = task / 3, r = task - 3 * u;
+    uint4 o = expand_role(T, K, L, in_s[off + u], in_t[off + u], r, pm1, tb_mask);
+    if (r < 2) {
+      out_s[2 * u + r] = o;
+    } else {
+      out_t[2 * u] = o.x & tmask;
+      out_t[2 * u + 1] = (o.x >> pm1) & tmask;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_key_prep: raw key bytes -> DevKey (one workgroup per key)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_key_prep(const uint8_t* __restrict__ raw,
+                                                  size_t key_stride, int p, int n, int nq,
+                                                  int party0, DevKey* __restrict__ out) {
+  const uint8_t* key = raw + blockIdx.x * key_stride;
+  DevKey* K = out + blockIdx.x;
+  const int pm1 = p - 1, CWk = 16 + 2 * p - 2, CW = pm1 * CWk;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    uint32_t w[4];
+    for (int i = 0; i < 4; ++i)
+      w[i] = key[4 * i] | (key[4 * i + 1] << 8) | (key[4 * i + 2] << 16) | ((uint32_t)key[4 * i + 3] << 24);
+    K->root_seed = make_uint4(w[0], w[1], w[2], w[3]);
+    K->root_t = party0 >= 1 ? (1u << (party0 - 1)) : 0u;
+    K->p = p; K->n = n; K->nq = nq;
+  }
+  for (int e = tid; e < n * pm1; e += blockDim.x) {
+    const int L = e / pm1, j = e - L * pm1;
+    const uint8_t* cw = key + 16 + L * CW + j * CWk;  // dpf_tree.cpp:506-513
+    uint32_t w[4];
+    for (int i = 0; i < 4; ++i)
+      w[i] = cw[4 * i] | (cw[4 * i + 1] << 8) | (cw[4 * i + 2] << 16) | ((uint32_t)cw[4 * i + 3] << 24);
+    K->scw[L * kMaxCW + j] = make_uint4(w[0], w[1], w[2], w[3]);
+    uint32_t tb = 0;
+    for (int k = 0; k < 2 * pm1; ++k) tb |= (uint32_t)(cw[16 + k] & 1u) << k;
+    K->tcw[L * kMaxCW + j] = tb;
+  }
+  for (int j = tid; j < kMaxCW; j += blockDim.x) {  // dpf_tree.cpp:515-519
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (j < pm1)
+      for (int a = 0; a < nq; ++a)
+        w[a >> 2] |= (uint32_t)key[16 + n * CW + a * pm1 + j] << (8 * (a & 3));
+    K->lastcw[j] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_tree_frontier: each of 2^g workgroups descends from the root along
+// (prefix << g | blockIdx.x) for log_parts + g levels (3 lanes per node: one AES block
+// each), then expands e levels breadth-first in LDS; the last level goes to global memory.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kTreeThreads) void k_tree_frontier(
+    const DevKey* __restrict__ K, uint64_t prefix, int log_parts, int g, int e,
+    uint4* __restrict__ front_s, uint32_t* __restrict__ front_t) {
+  __shared__ TreeSmem sm;
+  load_te_lds(sm.te);
+  const Te T{reinterpret_cast<const char*>(sm.te), (threadIdx.x & 31u) * 4u};
+  const uint32_t pm1 = K->p - 1;
+  const uint32_t tbits = 2 * pm1;
+  const uint32_t tb_mask = tbits >= 32 ? 0xffffffffu : ((1u << tbits) - 1u);
+  if (threadIdx.x == 0) {
+    sm.s[0][0] = K->root_seed;
+    sm.t[0][0] = K->root_t;
+  }
+  __syncthreads();
+  const int D0 = log_parts + g;
+  const uint64_t path = (prefix << g) | blockIdx.x;
+  int cur = 0, pidx = 0;
+  for (int L = 0; L < D0; ++L) {  // descent (cf. the intended dpf_tree.cpp:657-684)
+    if (threadIdx.x < 3) {
+      const int r = threadIdx.x;
+      uint4 o = expand_role(T, K, L, sm.s[cur][pidx], sm.t[cur][pidx], r, pm1, tb_mask);
+      if (r < 2) {
+        sm.s[cur ^ 1][r] = o;
+      } else {
+        const uint32_t tmask = (1u << pm1) - 1u;
+        sm.t[cur ^ 1][0] = o.x & tmask;
+        sm.t[cur ^ 1][1] = (o.x >> pm1) & tmask;
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+    pidx = (int)((path >> (D0 - 1 - L)) & 1u);
+  }
+  const uint64_t base = (uint64_t)blockIdx.x << e;
+  if (e == 0) {
+    if (threadIdx.x == 0) {
+      front_s[blockIdx.x] = sm.s[cur][pidx];
+      front_t[blockIdx.x] = sm.t[cur][pidx];
+    }
+    return;
+  }
+  int W = 1, off = pidx;
+  for (int lv = 0; lv < e; ++lv) {
+    const int L = D0 + lv;
+    if (lv == e - 1) {
+      expand_level(T, K, L, sm.s[cur], sm.t[cur], off, W, front_s + base, front_t + base, pm1,
+                   tb_mask);
+    } else {
+      expand_level(T, K, L, sm.s[cur], sm.t[cur], off, W, sm.s[cur ^ 1], sm.t[cur ^ 1], pm1,
+                   tb_mask);
+      __syncthreads();
+      cur ^= 1;
+      W *= 2;
+      off = 0;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_tree_leaves: `tile` frontier nodes per workgroup, d more levels in LDS, then every leaf
+// j gives c[j][a] = AES_{s_j}(0)[a] ^ XOR_{k: t_j bit k} lastCW[k][a]  (dpf_tree.cpp:567-580)
+// c layout: row-major [leaf][nrp] bytes (nrp = pow2 >= nq, unused bytes zero).
+// ------------------------------------------------------------------------------------------
+template <int NRP>
+__global__ __launch_bounds__(kTreeThreads) void k_tree_leaves(
+    const DevKey* __restrict__ K, const uint4* __restrict__ front_s,
+    const uint32_t* __restrict__ front_t, int L0, int d, int tile, uint8_t* __restrict__ c) {
+  __shared__ TreeSmem sm;
+  load_te_lds(sm.te);
+  const Te T{reinterpret_cast<const char*>(sm.te), (threadIdx.x & 31u) * 4u};
+  const uint32_t pm1 = K->p - 1;
+  const uint32_t tbits = 2 * pm1;
+  const uint32_t tb_mask = tbits >= 32 ? 0xffffffffu : ((1u << tbits) - 1u);
+  const uint64_t fbase = (uint64_t)blockIdx.x * tile;
+  for (int i = threadIdx.x; i < tile; i += blockDim.x) {
+    sm.s[0][i] = front_s[fbase + i];
+    sm.t[0][i] = front_t[fbase + i];
+  }
+  __syncthreads();
+  int cur = 0, W = tile;
+  for (int lv = 0; lv < d; ++lv) {
+    expand_level(T, K, L0 + lv, sm.s[cur], sm.t[cur], 0, W, sm.s[cur ^ 1], sm.t[cur ^ 1], pm1,
+                 tb_mask);
+    __syncthreads();
+    cur ^= 1;
+    W *= 2;
+  }
+  const uint32_t nq = K->nq;
+  uint4 qmask;  // keep bytes a < nq
+  {
+    uint32_t m[4];
+    for (int w = 0; w < 4; ++w) {
+      const int lo = 4 * w;
+      const int nb = (int)nq - lo;
+      m[w] = nb >= 4 ? 0xffffffffu : (nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u));
+    }
+    qmask = make_uint4(m[0], m[1], m[2], m[3]);
+  }
+  const uint64_t lbase = fbase << d;
+  for (int i = threadIdx.x; i < W; i += blockDim.x) {
+    uint4 o = aes_ctr_block(T, sm.s[cur][i], 0u);
+    const uint32_t t = sm.t[cur][i];
+    for (uint32_t j = 0; j < pm1; ++j) o = xor4(o, and4(K->lastcw[j], 0u - ((t >> j) & 1u)));
+    o = make_uint4(o.x & qmask.x, o.y & qmask.y, o.z & qmask.z, o.w & qmask.w);
+    uint8_t* dst = c + (lbase + i) * NRP;
+    if constexpr (NRP == 1) {
+      *dst = (uint8_t)o.x;
+    } else if constexpr (NRP == 2) {
+      *reinterpret_cast<uint16_t*>(dst) = (uint16_t)o.x;
+    } else if constexpr (NRP == 4) {
+      *reinterpret_cast<uint32_t*>(dst) = o.x;
+    } else if constexpr (NRP == 8) {
+      *reinterpret_cast<uint2*>(dst) = make_uint2(o.x, o.y);
+    } else {
+      *reinterpret_cast<uint4*>(dst) = o;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_scan: per-workgroup partial answers over GF(2^8), poly 0x11d (coding.cpp:9-21)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t gf_xtime4(uint32_t x) {  // 4 packed bytes times alpha
+  return ((x & 0x7f7f7f7fu) << 1) ^ (((x >> 7) & 0x01010101u) * 0x1du);
+}
+
+template <int VEC>
+struct Chunk {
+  uint32_t v[VEC];
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <int VEC>
+__device__ __forceinline__ Chunk<VEC> load_chunk(const uint8_t* p) {
+  Chunk<VEC> ch;
+  if constexpr (VEC == 4) {
+    u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    ch.v[0] = q.x; ch.v[1] = q.y; ch.v[2] = q.z; ch.v[3] = q.w;
+  } else if constexpr (VEC == 2) {
+    u32x2 q = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
+    ch.v[0] = q.x; ch.v[1] = q.y;
+  } else {
+    ch.v[0] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
+  }
+  return ch;
+}
+
+// coefficient bytes of record i: nrp bytes at c + i*nrp, as 4 dwords
+template <int NRP>
+__device__ __forceinline__ uint4 load_coef(const uint8_t* c, uint64_t i) {
+  if constexpr (NRP == 1) return make_uint4(c[i], 0, 0, 0);
+  else if constexpr (NRP == 2) return make_uint4(reinterpret_cast<const uint16_t*>(c)[i], 0, 0, 0);
+  else if constexpr (NRP == 4) return make_uint4(reinterpret_cast<const uint32_t*>(c)[i], 0, 0, 0);
+  else if constexpr (NRP == 8) {
+    uint2 q = reinterpret_cast<const uint2*>(c)[i];
+    return make_uint4(q.x, q.y, 0, 0);
+  } else {
+    return reinterpret_cast<const uint4*>(c)[i];
+  }
+}
+
+__device__ __forceinline__ uint32_t coef_byte(const uint4& c, int a) {
+  const uint32_t w = a < 4 ? c.x : (a < 8 ? c.y : (a < 12 ? c.z : c.w));
+  return (w >> (8 * (a & 3))) & 0xffu;
+}
+
+template <int NQ, int NRP, int VEC, bool UNI>
+__global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict__ shard,
+                                                       uint64_t nrec, uint32_t pitch,
+                                                       uint32_t cpr, const uint8_t* __restrict__ c,
+                                                       uint8_t* __restrict__ slabs) {
+  constexpr int CH = VEC * 4;  // bytes per lane chunk
+  constexpr int GW = kColGroupLanes * VEC;  // words per column group
+  __shared__ uint32_t red[NQ * GW];
+  for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) red[i] = 0;
+
+  const int lane = threadIdx.x & 63;
+  const uint32_t waves_per_block = blockDim.x >> 6;
+  const uint64_t wave = (uint64_t)blockIdx.x * waves_per_block + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * waves_per_block;
+  uint32_t rpw, rec_off, chunk;
+  bool active;
+  if (UNI) {
+    rpw = 1; rec_off = 0;
+    chunk = blockIdx.y * kColGroupLanes + lane;
+    active = chunk < cpr;
+  } else {
+    rpw = kColGroupLanes / cpr;
+    rec_off = lane / cpr;
+    chunk = lane - rec_off * cpr;
+    active = (uint32_t)lane < rpw * cpr;
+  }
+  const uint64_t ngroups = (nrec + rpw - 1) / rpw;
+  const uint64_t g0 = wave * ngroups / nwaves, g1 = (wave + 1) * ngroups / nwaves;
+
+  uint32_t Z[NQ][8][VEC];
+#pragma unroll
+  for (int a = 0; a < NQ; ++a)
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) Z[a][k][v] = 0;
+
+  const uint8_t* base = shard + (uint64_t)chunk * CH;
+  constexpr int U = 4;
+  uint64_t gi = g0;
+  for (; gi + U <= g1; gi += U) {
+    Chunk<VEC> x[U];
+    uint4 cf[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t rec = (gi + u) * rpw + rec_off;
+      const bool ok = active && rec < nrec;
+      if (ok) x[u] = load_chunk<VEC>(base + rec * pitch);
+      else
+        for (int v = 0; v < VEC; ++v) x[u].v[v] = 0;
+      if (UNI) {
+        const uint64_t r = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(gi + u)) |
+                           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((gi + u) >> 32)) << 32);
+        cf[u] = load_coef<NRP>(c, r);
+      } else {
+        cf[u] = ok ? load_coef<NRP>(c, rec) : make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int a = 0; a < NQ; ++a) {
+        const uint32_t ca = coef_byte(cf[u], a);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t m = 0u - ((ca >> k) & 1u);
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) Z[a][k][v] ^= x[u].v[v] & m;
+        }
+      }
+  }
+  for (; gi < g1; ++gi) {
+    const uint64_t rec = gi * rpw + rec_off;
+    const bool ok = active && rec < nrec;
+    Chunk<VEC> x;
+    if (ok) x = load_chunk<VEC>(base + rec * pitch);
+    else
+      for (int v = 0; v < VEC; ++v) x.v[v] = 0;
+    const uint4 cf = ok ? load_coef<NRP>(c, rec) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int a = 0; a < NQ; ++a) {
+      const uint32_t ca = coef_byte(cf, a);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t m = 0u - ((ca >> k) & 1u);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) Z[a][k][v] ^= x.v[v] & m;
+      }
+    }
+  }
+  __syncthreads();  // red[] zeroed
+  if (active) {
+    const uint32_t wbase = (UNI ? (uint32_t)lane : chunk) * VEC;
+#pragma unroll
+    for (int a = 0; a < NQ; ++a)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        uint32_t acc = Z[a][7][v];
+#pragma unroll
+        for (int k = 6; k >= 0; --k) acc = gf_xtime4(acc) ^ Z[a][k][v];
+        if (acc) atomicXor(&red[a * GW + wbase + v], acc);
+      }
+  }
+  __syncthreads();
+  uint32_t* slab = reinterpret_cast<uint32_t*>(slabs) +
+                   ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * (NQ * GW);
+  for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) slab[i] = red[i];
+}
+
+// slabs: [grid.y][grid.x][nq][GW words]; out[a*efs + b] for b < efs
+__global__ void k_reduce(const uint32_t* __restrict__ slabs, int nq, uint32_t gw, uint32_t gx,
+                         uint32_t gy, uint32_t pitch, uint32_t efs, uint8_t* __restrict__ out) {
+  const uint32_t words = pitch / 4;
+  const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (uint32_t)nq * words) return;
+  const uint32_t a = idx / words, w = idx - a * words;
+  const uint32_t grp = w / gw, win = w - grp * gw;
+  const uint32_t* p = slabs + ((uint64_t)grp * gx) * nq * gw + (uint64_t)a * gw + win;
+  uint32_t acc = 0;
+  for (uint32_t x = 0; x < gx; ++x) acc ^= p[(uint64_t)x * nq * gw];
+  const uint32_t b0 = 4 * w;
+  uint8_t* dst = out + (uint64_t)a * efs;
+  if ((efs & 3u) == 0 && b0 + 4 <= efs) {
+    *reinterpret_cast<uint32_t*>(dst + b0) = acc;
+  } else {
+    for (uint32_t k = 0; k < 4; ++k)
+      if (b0 + k < efs) dst[b0 + k] = (uint8_t)(acc >> (8 * k));
+  }
+  (void)gy;
+}
+
+__global__ void k_xor_fold(const uint8_t* __restrict__ in, int nranks, size_t len,
+                           uint8_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= len) return;
+  uint8_t acc = 0;
+  for (int r = 0; r < nranks; ++r) acc ^= in[(size_t)r * len + i];
+  out[i] = acc;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void k_fill_random(uint8_t* __restrict__ d, size_t bytes, uint64_t seed) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < bytes) d[i] = (uint8_t)splitmix64(seed ^ (i * 0xD1B54A32D192ED03ull));
+}
+
+// byte b of global row i = byte (b & 7) of splitmix64(seed ^ (i << 20 | b >> 3)); padding 0
+__global__ void k_fill_shard(uint8_t* __restrict__ shard, uint64_t rows, uint32_t pitch,
+                             uint32_t efs, uint64_t row0, uint64_t seed) {
+  const uint32_t cpr = pitch / 16;
+  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * cpr) return;
+  const uint64_t r = idx / cpr;
+  const uint32_t ch = (uint32_t)(idx - r * cpr);
+  const uint64_t gr = row0 + r;
+  uint32_t w[4];
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t b = ch * 16 + h * 8;
+    const uint64_t z = splitmix64(seed ^ ((gr << 20) | (b >> 3)));
+    w[2 * h] = (uint32_t)z;
+    w[2 * h + 1] = (uint32_t)(z >> 32);
+  }
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t b = ch * 16 + k;
+    if (b >= efs) w[k >> 2] &= ~(0xffu << (8 * (k & 3)));
+  }
+  *reinterpret_cast<uint4*>(shard + r * pitch + ch * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// ------------------------------------------------------------------------------------------
+// host side: tables, plans, launchers
+// ------------------------------------------------------------------------------------------
+TreePlan make_plan(int n, int log_parts, uint64_t prefix) {
+  TreePlan pl{};
+  pl.n = n;
+  pl.log_parts = log_parts;
+  pl.prefix = prefix;
+  const int nr = n - log_parts;  // depth of this partition's subtree
+  pl.d = std::min(nr, 3);
+  const int F = nr - pl.d;       // frontier depth below the partition root
+  // frontier kernel: 2^g workgroups (about two per CU), each expanding e <= 11 levels
+  int g = std::min(F, 9);
+  if (F - g > 11) g = F - 11;
+  pl.g = g;
+  pl.e = F - g;
+  pl.nfront = 1ull << F;
+  pl.tile = (int)std::min<uint64_t>(pl.nfront, (uint64_t)(kNodeCap >> pl.d));
+  pl.nleaves = 1ull << nr;
+  return pl;
+}
+
+hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys, int p, int n,
+                           int nq, int party0, DevKey* d_keys, hipStream_t s) {
+  hipLaunchKernelGGL(k_key_prep, dim3(num_keys), dim3(256), 0, s, d_raw, key_stride, p, n, nq,
+                     party0, d_keys);
+  return hipGetLastError();
+}
+
+hipError_t launch_tree(const TreePlan& pl, const DevKey* d_key, uint4* d_front_s,
+                       uint32_t* d_front_t, uint8_t* d_c, int nrp, hipStream_t s,
+                       hipEvent_t mid) {
+  hipLaunchKernelGGL(k_tree_frontier, dim3(1u << pl.g), dim3(kTreeThreads), 0, s, d_key,
+                     pl.prefix, pl.log_parts, pl.g, pl.e, d_front_s, d_front_t);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return err;
+  if (mid) (void)hipEventRecord(mid, s);
+  const int L0 = pl.log_parts + pl.g + pl.e;
+  const dim3 grid((unsigned)(pl.nfront / pl.tile));
+  switch (nrp) {
+    case 1: hipLaunchKernelGGL(k_tree_leaves<1>, grid, dim3(kTreeThreads), 0, s, d_key, d_front_s, d_front_t, L0, pl.d, pl.tile, d_c); break;
+    case 2: hipLaunchKernelGGL(k_tree_leaves<2>, grid, dim3(kTreeThreads), 0, s, d_key, d_front_s, d_front_t, L0, pl.d, pl.tile, d_c); break;
+    case 4: hipLaunchKernelGGL(k_tree_leaves<4>, grid, dim3(kTreeThreads), 0, s, d_key, d_front_s, d_front_t, L0, pl.d, pl.tile, d_c); break;
+    case 8: hipLaunchKernelGGL(k_tree_leaves<8>, grid, dim3(kTreeThreads), 0, s, d_key, d_front_s, d_front_t, L0, pl.d, pl.tile, d_c); break;
+    case 16: hipLaunchKernelGGL(k_tree_leaves<16>, grid, dim3(kTreeThreads), 0, s, d_key, d_front_s, d_front_t, L0, pl.d, pl.tile, d_c); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+static int vec_for(int nq) { return nq <= 2 ? 4 : (nq <= 8 ? 2 : 1); }
+
+ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus) {
+  ScanShape sh{};
+  sh.nq = nq;
+  sh.nrp = nq == 1 ? 1 : (nq == 2 ? 2 : (nq <= 4 ? 4 : (nq <= 8 ? 8 : 16)));
+  sh.vec = vec_for(nq);
+  sh.pitch = pitch;
+  sh.cpr = pitch / (sh.vec * 4);
+  sh.uniform = sh.cpr >= (uint32_t)kColGroupLanes;
+  const uint32_t gy = sh.uniform ? (sh.cpr + kColGroupLanes - 1) / kColGroupLanes : 1;
+  const uint32_t rpw = sh.uniform ? 1 : kColGroupLanes / sh.cpr;
+  const uint64_t groups = (nrec + rpw - 1) / rpw;
+  // enough waves to keep ~64 KiB of loads in flight per CU, at least a few groups per wave
+  const uint64_t want_blocks = (uint64_t)num_cus * 8;
+  const uint64_t waves_per_block = kScanThreads / 64;
+  uint64_t gx = std::max<uint64_t>(1, std::min<uint64_t>(want_blocks / gy, (groups + 4 * waves_per_block - 1) / (4 * waves_per_block)));
+  sh.grid = dim3((unsigned)gx, gy);
+  sh.slab_bytes = (uint32_t)(nq * kColGroupLanes * sh.vec * 4);
+  return sh;
+}
+
+template <int NQ>
+static hipError_t scan_nq(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
+                          const uint8_t* d_c, uint8_t* d_slabs, hipStream_t s) {
+  constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : (NQ <= 8 ? 8 : 16)));
+  constexpr int VEC = NQ <= 2 ? 4 : (NQ <= 8 ? 2 : 1);
+  if (sh.uniform)
+    hipLaunchKernelGGL((k_scan<NQ, NRP, VEC, true>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
+                       nrec, sh.pitch, sh.cpr, d_c, d_slabs);
+  else
+    hipLaunchKernelGGL((k_scan<NQ, NRP, VEC, false>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
+                       nrec, sh.pitch, sh.cpr, d_c, d_slabs);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
+                       const uint8_t* d_c, uint8_t* d_slabs, hipStream_t s) {
+  switch (sh.nq) {
+    case 1: return scan_nq<1>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 2: return scan_nq<2>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 3: return scan_nq<3>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 4: return scan_nq<4>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 5: return scan_nq<5>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 6: return scan_nq<6>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 7: return scan_nq<7>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 8: return scan_nq<8>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 9: return scan_nq<9>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 10: return scan_nq<10>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 11: return scan_nq<11>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 12: return scan_nq<12>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 13: return scan_nq<13>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 14: return scan_nq<14>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 15: return scan_nq<15>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 16: return scan_nq<16>(sh, d_shard, nrec, d_c, d_slabs, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t efs,
+                         uint8_t* d_out, hipStream_t s) {
+  const uint32_t words = sh.pitch / 4;
+  const uint32_t total = (uint32_t)sh.nq * words;
+  const uint32_t gw = kColGroupLanes * sh.vec;
+  hipLaunchKernelGGL(k_reduce, dim3((total + 255) / 256), dim3(256), 0, s,
+                     reinterpret_cast<const uint32_t*>(d_slabs), sh.nq, gw, sh.grid.x, sh.grid.y,
+                     sh.pitch, efs, d_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_xor_fold(const uint8_t* d_in, int nranks, size_t len, uint8_t* d_out,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_xor_fold, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, d_in,
+                     nranks, len, d_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_random(uint8_t* d, size_t bytes, uint64_t seed, hipStream_t s) {
+  hipLaunchKernelGGL(k_fill_random, dim3((unsigned)((bytes + 255) / 256)), dim3(256), 0, s, d,
+                     bytes, seed);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_shard(uint8_t* d_shard, uint64_t rows, uint32_t pitch, uint32_t efs,
+                             uint64_t global_row0, uint64_t seed, hipStream_t s) {
+  const uint64_t total = rows * (pitch / 16);
+  hipLaunchKernelGGL(k_fill_shard, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                     d_shard, rows, pitch, efs, global_row0, seed);
+  return hipGetLastError();
+}
+
+}  // namespace pir

@@ -1,0 +1,283 @@
+// pir_server.cpp -- the server.h / params.h / client.h-compatible shim (include/pir_server.h)
+// over the MI355X engine.  Host glue only: every answer is computed by the HIP kernels behind
+// pir_engine_answer / pir_engine_answer_slice.
+#include "../../include/pir_server.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/pir_engine.h"
+
+extern "C" {
+int NUM_PARTIES = 0;
+int NUM_FILES = 0;
+uint32_t LOG_NUM_FILES = 0;
+uint32_t FILE_SIZE_BYTES = 0;
+uint32_t PAYLOAD_SIZE_BYTES = 0;
+int NUM_ENCODED_FILES = 0;
+int LOG_NUM_ENCODED_FILES = 0;
+int ENCODED_PAYLOAD_SIZE_BYTES = 0;
+int ENCODED_FILE_SIZE_BYTES = 0;
+int ENCODE_ACROSS = -1;
+int NUM_ROUNDS = 0;
+int RHO = 2;
+int K = 0;
+int T = 0;
+int R = 0;
+int B = 0;
+int NUM_RESPONSES = 0;
+int MODE = -1;
+int IS_HERMITE = 0;
+int D = 0;
+int MAC_SIZE_BYTES = 32;
+int CHECK_MAC = 0;
+}
+
+namespace {
+
+int g_device = -1;
+
+int device_default() {
+  if (g_device >= 0) return g_device;
+  const char* s = getenv("PIR_DEVICE");
+  return s ? atoi(s) : 0;
+}
+
+[[noreturn]] void die(const char* what) {
+  fprintf(stderr, "pir engine failure in %s: %s\n", what, pir_engine_last_error());
+  abort();  // the reference's handleErrors() (utils.cpp:11-15)
+}
+
+// Per-server engine state, hung off server.ctx.
+struct ShimState {
+  std::mutex mu;
+  pir_engine_t* eng = nullptr;
+  pir_engine_config cfg{};
+  bool dirty = true;  // indexList changed since the last upload
+  uint32_t rows_alloc = 0;
+};
+
+ShimState* state_of(server* s) {
+  if (!s || !s->ctx) {
+    fprintf(stderr, "pir shim: query on an uninitialised or freed server\n");
+    abort();
+  }
+  return static_cast<ShimState*>(s->ctx);
+}
+
+// Make sure the engine matches the current globals / nq and holds the current indexList.
+pir_engine_t* engine_for(server* s, ShimState* st, int nq) {
+  pir_engine_config c{};
+  c.device = device_default();
+  c.num_parties = NUM_PARTIES;
+  c.party_index = s->partyIndex;
+  c.log_num_records = LOG_NUM_ENCODED_FILES;
+  c.record_bytes = (uint32_t)ENCODED_FILE_SIZE_BYTES;
+  c.num_rounds = nq;
+  c.log_num_partitions = 0;
+  c.partition_index = 0;
+  c.is_byzantine = s->isByzantine;
+  if (!st->eng || memcmp(&c, &st->cfg, sizeof c) != 0) {
+    if (st->eng) pir_engine_destroy(st->eng);
+    st->eng = nullptr;
+    if (pir_engine_create(&c, &st->eng) != PIR_OK) die("pir_engine_create");
+    st->cfg = c;
+    st->dirty = true;
+  }
+  if (st->dirty) {
+    const uint64_t n = 1ull << c.log_num_records;
+    if (n > st->rows_alloc) {
+      fprintf(stderr, "pir shim: %llu encoded rows but the server holds %u\n",
+              (unsigned long long)n, st->rows_alloc);
+      abort();
+    }
+    if (pir_engine_set_shard_rows(st->eng, s->indexList, 0, n) != PIR_OK)
+      die("pir_engine_set_shard_rows");
+    st->dirty = false;
+  }
+  return st->eng;
+}
+
+int ceil_log2(long v) {
+  int l = 0;
+  while ((1L << l) < v) ++l;
+  return l;
+}
+
+uint8_t gf_mul_h(uint8_t a, uint8_t b) {  // 0x11d field (coding.cpp:9-21), carry-less form
+  uint8_t r = 0;
+  while (b) {
+    if (b & 1) r ^= a;
+    a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1d : 0));
+    b >>= 1;
+  }
+  return r;
+}
+
+uint8_t gf_pow_h(uint8_t base, int exp) {  // coding.cpp:46-60 (pow(0, e) == 1 there, too)
+  if (base == 0) return 1;
+  uint8_t r = 1;
+  for (int i = 0; i < exp; ++i) r = gf_mul_h(r, base);
+  return r;
+}
+
+}  // namespace
+
+extern "C" {
+
+void pirSetDevice(int device) { g_device = device; }
+
+void pirServerShardChanged(server* s) {
+  if (s && s->ctx) static_cast<ShimState*>(s->ctx)->dirty = true;
+}
+
+int calcOptimizedDPFTreeKeyLength(int p, int log_domainSize, int numQueries) {
+  return pir_engine_key_len(p, log_domainSize, numQueries);
+}
+
+// params.cpp:467-512 with setModeParams(Tree) (params.cpp:414-418)
+void setSystemParams(int logNumFiles, int fileSizeBytes, int t, int k, int r, int b, int rho,
+                     int checkMac, int mode) {
+  if (mode != 0) {
+    fprintf(stderr, "pir shim: mode %d is outside the tree-DPF engine's scope\n", mode);
+    abort();
+  }
+  if (t != 1) {  // params.cpp:415 assert(T == 1)
+    fprintf(stderr, "pir shim: tree mode requires t == 1 (got %d)\n", t);
+    abort();
+  }
+  RHO = rho; K = k; T = t; R = r; B = b;
+  NUM_FILES = 1 << logNumFiles;
+  LOG_NUM_FILES = (uint32_t)logNumFiles;
+  PAYLOAD_SIZE_BYTES = (uint32_t)fileSizeBytes;
+  FILE_SIZE_BYTES = (uint32_t)fileSizeBytes;
+  CHECK_MAC = checkMac;
+  MODE = mode;
+  NUM_PARTIES = K + R + T + 2 * B + (RHO - 1);
+  ENCODE_ACROSS = 1;
+  NUM_RESPONSES = NUM_PARTIES - R;
+  LOG_NUM_ENCODED_FILES = ceil_log2((NUM_FILES + k - 1) / k);
+  NUM_ENCODED_FILES = 1 << LOG_NUM_ENCODED_FILES;
+  ENCODED_PAYLOAD_SIZE_BYTES = (int)FILE_SIZE_BYTES;
+  ENCODED_FILE_SIZE_BYTES = (int)FILE_SIZE_BYTES;
+  if (CHECK_MAC) {
+    FILE_SIZE_BYTES += MAC_SIZE_BYTES;
+    ENCODED_FILE_SIZE_BYTES += MAC_SIZE_BYTES;
+  }
+  NUM_ROUNDS = (K == 1) ? 1 : K / RHO;
+}
+
+void freeParams(void) {}
+
+// server.cpp:17-42: rows are host memory the Go setup path encodes into; the engine (and the
+// device copy of the shard) is created on the first query.
+void initializeServer(server* s, int partyIndex, uint32_t logNumFiles, uint32_t fileSizeBytes,
+                      int isByzantine, int numThreads) {
+  auto* st = new ShimState;
+  s->ctx = st;
+  s->ctxThreads = nullptr;
+  s->partyIndex = partyIndex;
+  const uint32_t n = 1u << logNumFiles;
+  s->indexList = (uint8_t**)malloc((size_t)n * sizeof(uint8_t*));
+  for (uint32_t i = 0; i < n; ++i) s->indexList[i] = (uint8_t*)calloc(fileSizeBytes, 1);
+  st->rows_alloc = n;
+  s->isByzantine = isByzantine;
+  s->numThreads = numThreads;
+}
+
+// server.cpp:45-52
+void freeServer(server* s) {
+  if (!s || !s->ctx) return;
+  ShimState* st = static_cast<ShimState*>(s->ctx);
+  if (st->eng) pir_engine_destroy(st->eng);
+  for (uint32_t i = 0; i < st->rows_alloc; ++i) free(s->indexList[i]);
+  free(s->indexList);
+  s->indexList = nullptr;
+  delete st;
+  s->ctx = nullptr;
+}
+
+// server.cpp:96-134
+void runOptimizedDPFTreeQuery(server* s, uint8_t* key, int numQueries, uint8_t** result) {
+  ShimState* st = state_of(s);
+  std::lock_guard<std::mutex> lk(st->mu);
+  pir_engine_t* e = engine_for(s, st, numQueries);
+  const size_t efs = (size_t)ENCODED_FILE_SIZE_BYTES;
+  std::vector<uint8_t> out((size_t)numQueries * efs);
+  if (pir_engine_answer(e, key, out.data()) != PIR_OK) die("runOptimizedDPFTreeQuery");
+  for (int a = 0; a < numQueries; ++a) memcpy(result[a], out.data() + a * efs, efs);
+}
+
+// server.cpp:505-549, intended semantics (see pir_server.h)
+void runOptimizedDPFTreeQueryThread(server* s, uint8_t* key, int threadNum, int numThreads,
+                                    uint8_t** result) {
+  ShimState* st = state_of(s);
+  std::lock_guard<std::mutex> lk(st->mu);
+  pir_engine_t* e = engine_for(s, st, NUM_ROUNDS);
+  const size_t efs = (size_t)ENCODED_FILE_SIZE_BYTES;
+  std::vector<uint8_t> out((size_t)NUM_ROUNDS * efs);
+  if (pir_engine_answer_slice(e, key, threadNum, numThreads, out.data()) != PIR_OK)
+    die("runOptimizedDPFTreeQueryThread");
+  for (int a = 0; a < NUM_ROUNDS; ++a) memcpy(result[a], out.data() + a * efs, efs);
+}
+
+// server.cpp:553-562 (host buffers from the Go caller)
+void assemblDPFTreeQueryThreadResults(server* s, uint8_t*** in, int numThreads, uint8_t** out) {
+  (void)s;
+  for (int a = 0; a < NUM_ROUNDS; ++a) {
+    memset(out[a], 0, ENCODED_FILE_SIZE_BYTES);
+    for (int t = 0; t < numThreads; ++t)
+      for (int j = 0; j < ENCODED_FILE_SIZE_BYTES; ++j) out[a][j] ^= in[t][a][j];
+  }
+}
+
+// client.cpp:16-33 (synthetic DB; MAC tags are outside this engine's scope)
+void initialize_client(client* c, uint8_t log_num_files, uint32_t file_size_bytes) {
+  (void)file_size_bytes;
+  if (CHECK_MAC) {
+    fprintf(stderr, "pir shim: CHECK_MAC setups are outside the engine's scope\n");
+    abort();
+  }
+  c->ctx = nullptr;
+  c->macCtx = nullptr;
+  c->macKey = (uint8_t*)"1234567812345678";
+  const uint32_t n = 1u << log_num_files;
+  c->unencoded_files = (uint8_t**)malloc((size_t)n * sizeof(uint8_t*));
+  for (uint32_t i = 0; i < n; ++i) {
+    c->unencoded_files[i] = (uint8_t*)malloc(FILE_SIZE_BYTES);
+    memset(c->unencoded_files[i], (int)(i & 0xff), PAYLOAD_SIZE_BYTES);
+    if (i == 1)
+      for (uint32_t j = 0; j < PAYLOAD_SIZE_BYTES; ++j) c->unencoded_files[i][j] = (uint8_t)j;
+  }
+}
+
+void free_client(client* c) {  // client.cpp:35-41
+  for (int i = 0; i < NUM_FILES; ++i) free(c->unencoded_files[i]);
+  free(c->unencoded_files);
+  c->unencoded_files = nullptr;
+}
+
+// client.cpp:70-97: row i of party q = XOR_j gf_pow(q, j) * file[encDBsize*j + i]
+void encode_across_files_server(client* c, server* s) {
+  const long encdb = (NUM_FILES + K - 1) / K;
+  const int efs = ENCODED_FILE_SIZE_BYTES;
+  std::vector<uint8_t> coef(K);
+  for (int j = 0; j < K; ++j) coef[j] = gf_pow_h((uint8_t)s->partyIndex, j);
+  for (int i = 0; i < NUM_ENCODED_FILES; ++i) {
+    uint8_t* row = s->indexList[i];
+    for (int j = 0; j < K; ++j) {
+      const long src = encdb * j + i;
+      if (src >= NUM_FILES) continue;
+      const uint8_t* f = c->unencoded_files[src];
+      for (int b = 0; b < efs; ++b) row[b] ^= gf_mul_h(f[b], coef[j]);
+    }
+  }
+  if (s->ctx) static_cast<ShimState*>(s->ctx)->dirty = true;
+}
+
+}  // extern "C"

@@ -1,0 +1,177 @@
+"""Python host mirror of the engine C ABI (include/pir_engine.h).
+
+`Engine` is one PIR server's shard -- or one 2^-G partition of it -- resident in the HBM of one
+MI355X, answering tree-DPF queries with the HIP kernels of csrc/pir_kernels.hip.  Method names
+follow the reference's server operations (src/c/server.h:27-53):
+
+    Engine.answer        runOptimizedDPFTreeQuery        (src/c/server.cpp:96-134)
+    Engine.answer_slice  runOptimizedDPFTreeQueryThread  (src/c/server.cpp:505-549, intended)
+    Engine.eval_all      evalAllOptimizedDPF             (src/c/dpf_tree.cpp:473-598)
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+
+def _buf(b):
+    if isinstance(b, (bytes, bytearray)):
+        b = np.frombuffer(bytes(b), dtype=np.uint8)
+    b = np.ascontiguousarray(b, dtype=np.uint8)
+    return b, b.ctypes.data_as(ctypes.c_void_p)
+
+
+def key_len(num_parties, log_num_records, num_rounds):
+    """calcOptimizedDPFTreeKeyLength (src/c/utils.cpp:85-90)."""
+    return _lib.load().pir_engine_key_len(num_parties, log_num_records, num_rounds)
+
+
+class Engine:
+    def __init__(self, num_parties, party_index, log_num_records, record_bytes, num_rounds=1,
+                 device=0, log_num_partitions=0, partition_index=0, is_byzantine=False):
+        lib = _lib.load()
+        self._lib = lib
+        cfg = _lib.PirConfig(device, num_parties, party_index, log_num_records, record_bytes,
+                             num_rounds, log_num_partitions, partition_index, int(is_byzantine))
+        h = ctypes.c_void_p()
+        check(lib.pir_engine_create(ctypes.byref(cfg), ctypes.byref(h)), "pir_engine_create")
+        self._h = h
+        self.num_parties = num_parties
+        self.party_index = party_index
+        self.n = log_num_records
+        self.record_bytes = record_bytes
+        self.num_rounds = num_rounds
+        self.log_num_partitions = log_num_partitions
+        self.partition_index = partition_index
+        self.key_len = key_len(num_parties, log_num_records, num_rounds)
+        self.num_rows = int(lib.pir_engine_num_rows(h))
+        self.answer_bytes = num_rounds * record_bytes
+
+    # -- lifetime ------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.pir_engine_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- shard -----------------------------------------------------------------------------
+    def set_shard(self, rows, row0=0):
+        """rows: (nrows, record_bytes) uint8 array (or a flat buffer of whole rows)."""
+        arr = np.ascontiguousarray(rows, dtype=np.uint8).reshape(-1, self.record_bytes)
+        check(self._lib.pir_engine_set_shard(self._h, arr.ctypes.data_as(ctypes.c_void_p), row0,
+                                             arr.shape[0], self.record_bytes),
+              "pir_engine_set_shard")
+
+    def fill_shard_random(self, seed):
+        check(self._lib.pir_engine_fill_shard_random(self._h, seed), "fill_shard_random")
+
+    def shard_row(self, i):
+        out = np.empty(self.record_bytes, np.uint8)
+        check(self._lib.pir_engine_get_shard_row(self._h, i, out.ctypes.data_as(ctypes.c_void_p)),
+              "get_shard_row")
+        return out
+
+    def get_shard(self, row0=0, nrows=None):
+        nrows = self.num_rows - row0 if nrows is None else nrows
+        out = np.empty((nrows, self.record_bytes), np.uint8)
+        check(self._lib.pir_engine_get_shard(self._h, row0, nrows,
+                                             out.ctypes.data_as(ctypes.c_void_p)), "get_shard")
+        return out
+
+    # -- answers ---------------------------------------------------------------------------
+    def _check_key(self, key):
+        k, kp = _buf(key)
+        if k.size != self.key_len:
+            raise ValueError(f"key has {k.size} bytes, expected {self.key_len}")
+        return k, kp
+
+    def answer(self, key):
+        """(num_rounds, record_bytes) answer of this engine (XOR over ranks if a comm is
+        attached)."""
+        k, kp = self._check_key(key)
+        out = np.empty((self.num_rounds, self.record_bytes), np.uint8)
+        check(self._lib.pir_engine_answer(self._h, kp, out.ctypes.data_as(ctypes.c_void_p)),
+              "pir_engine_answer")
+        return out
+
+    def answer_slice(self, key, thread_num, num_threads):
+        k, kp = self._check_key(key)
+        out = np.empty((self.num_rounds, self.record_bytes), np.uint8)
+        check(self._lib.pir_engine_answer_slice(self._h, kp, thread_num, num_threads,
+                                                out.ctypes.data_as(ctypes.c_void_p)),
+              "pir_engine_answer_slice")
+        return out
+
+    def eval_all(self, key):
+        """(num_rounds, rows) DPF shares dataShare[a][i]."""
+        k, kp = self._check_key(key)
+        out = np.empty((self.num_rounds, self.num_rows), np.uint8)
+        check(self._lib.pir_engine_eval_all(self._h, kp, out.ctypes.data_as(ctypes.c_void_p)),
+              "pir_engine_eval_all")
+        return out
+
+    # -- device-resident path ----------------------------------------------------------------
+    def alloc_dev(self, nbytes):
+        p = ctypes.c_void_p()
+        check(self._lib.pir_engine_alloc_dev(self._h, nbytes, ctypes.byref(p)), "alloc_dev")
+        return p.value
+
+    def h2d(self, d_ptr, host):
+        h, hp = _buf(host)
+        check(self._lib.pir_engine_memcpy_h2d(self._h, d_ptr, hp, h.size), "memcpy_h2d")
+
+    def d2h(self, d_ptr, nbytes):
+        out = np.empty(nbytes, np.uint8)
+        check(self._lib.pir_engine_memcpy_d2h(self._h, out.ctypes.data_as(ctypes.c_void_p),
+                                              d_ptr, nbytes), "memcpy_d2h")
+        return out
+
+    def answer_dev(self, d_key, d_result, stream=None):
+        check(self._lib.pir_engine_answer_dev(self._h, d_key, d_result, stream), "answer_dev")
+
+    def answer_batch_dev(self, d_keys, num_keys, d_result, stream=None):
+        check(self._lib.pir_engine_answer_batch_dev(self._h, d_keys, num_keys, d_result, stream),
+              "answer_batch_dev")
+
+    @property
+    def stream(self):
+        return self._lib.pir_engine_stream(self._h)
+
+    def sync(self):
+        check(self._lib.pir_engine_sync(self._h), "pir_engine_sync")
+
+    def set_profiling(self, slots=64):
+        """Record per-phase HIP events for up to `slots` answers (0 turns profiling off)."""
+        check(self._lib.pir_engine_set_profiling(self._h, int(slots)), "set_profiling")
+
+    def last_timings(self):
+        """{phase: mean ms} over the answers recorded since the previous call."""
+        arr = (_lib.PirKernelTime * 16)()
+        n = self._lib.pir_engine_last_timings(self._h, arr, 16)
+        if n < 0:
+            check(n, "last_timings")
+        return {arr[i].name.decode(): float(arr[i].ms) for i in range(n)}
+
+    # -- split shard ---------------------------------------------------------------------------
+    def attach_comm(self, unique_id, nranks, rank):
+        uid, up = _buf(unique_id)
+        check(self._lib.pir_comm_attach(self._h, up, nranks, rank), "pir_comm_attach")
+
+
+def comm_unique_id():
+    out = np.zeros(128, np.uint8)
+    check(_lib.load().pir_comm_unique_id(out.ctypes.data_as(ctypes.c_void_p)), "pir_comm_unique_id")
+    return out.tobytes()

@@ -1,0 +1,119 @@
+"""The reference's server-side API for the tree-DPF path, by its own names, over the
+server.h-compatible shim (include/pir_server.h) -- what the Go server binds through cgo
+(src/server_util/tree.go:65,76; src/server/server.go:299-331).  Parity tests use this module
+the way src/c/correctness_tests.cpp:230-372 drives src/c.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import CClient, CServer, c_u8_p
+
+
+def setSystemParams(logNumFiles, fileSizeBytes, t, k, r, b, rho, checkMac, mode):
+    _lib.load().setSystemParams(logNumFiles, fileSizeBytes, t, k, r, b, rho, checkMac, mode)
+
+
+def params():
+    """The sizing globals of src/c/params.h:9-33 as a dict."""
+    return {n: _lib.global_int(n) for n in _lib.GLOBALS_INT + _lib.GLOBALS_U32}
+
+
+def calcOptimizedDPFTreeKeyLength(p, log_domain_size, num_queries):
+    return _lib.load().calcOptimizedDPFTreeKeyLength(p, log_domain_size, num_queries)
+
+
+def _row_ptrs(arr2d):
+    rows = arr2d.shape[0]
+    base = arr2d.ctypes.data
+    ptrs = (c_u8_p * rows)()
+    for i in range(rows):
+        ptrs[i] = ctypes.cast(base + i * arr2d.strides[0], c_u8_p)
+    return ptrs
+
+
+class Server:
+    """A `server` struct (src/c/server.h:13-25) owned by the shim."""
+
+    def __init__(self, partyIndex, logNumFiles, fileSizeBytes, isByzantine=0, numThreads=1):
+        self._lib = _lib.load()
+        self.s = CServer()
+        self._lib.initializeServer(ctypes.byref(self.s), partyIndex, logNumFiles, fileSizeBytes,
+                                   isByzantine, numThreads)
+        self.rows = 1 << logNumFiles
+        self.file_size = fileSizeBytes
+
+    @property
+    def partyIndex(self):
+        return self.s.partyIndex
+
+    def write_rows(self, rows):
+        """Copy (nrows, file_size) bytes into indexList (as a test harness would) and tell the
+        shim the shard changed."""
+        rows = np.ascontiguousarray(rows, dtype=np.uint8).reshape(-1, self.file_size)
+        for i in range(rows.shape[0]):
+            ctypes.memmove(self.s.indexList[i], rows[i].ctypes.data, self.file_size)
+        self._lib.pirServerShardChanged(ctypes.byref(self.s))
+
+    def read_row(self, i):
+        return np.ctypeslib.as_array(self.s.indexList[i], (self.file_size,)).copy()
+
+    def runOptimizedDPFTreeQuery(self, key, numQueries):
+        efs = _lib.global_int("ENCODED_FILE_SIZE_BYTES")
+        out = np.zeros((numQueries, efs), np.uint8)
+        k = np.frombuffer(bytes(key), np.uint8).copy()
+        self._lib.runOptimizedDPFTreeQuery(ctypes.byref(self.s), k.ctypes.data_as(ctypes.c_void_p),
+                                           numQueries, _row_ptrs(out))
+        return out
+
+    def runOptimizedDPFTreeQueryThread(self, key, threadNum, numThreads):
+        efs = _lib.global_int("ENCODED_FILE_SIZE_BYTES")
+        nq = _lib.global_int("NUM_ROUNDS")
+        out = np.zeros((nq, efs), np.uint8)
+        k = np.frombuffer(bytes(key), np.uint8).copy()
+        self._lib.runOptimizedDPFTreeQueryThread(ctypes.byref(self.s),
+                                                 k.ctypes.data_as(ctypes.c_void_p), threadNum,
+                                                 numThreads, _row_ptrs(out))
+        return out
+
+    def freeServer(self):
+        if self.s.ctx:
+            self._lib.freeServer(ctypes.byref(self.s))
+
+    def __del__(self):
+        try:
+            self.freeServer()
+        except Exception:
+            pass
+
+
+def assemblDPFTreeQueryThreadResults(server, parts):
+    """parts: (numThreads, NUM_ROUNDS, EFS) -> (NUM_ROUNDS, EFS) (src/c/server.cpp:553-562)."""
+    parts = np.ascontiguousarray(parts, dtype=np.uint8)
+    T, nq, efs = parts.shape
+    ins = (ctypes.POINTER(c_u8_p) * T)()
+    keep = []
+    for t in range(T):
+        rp = _row_ptrs(parts[t])
+        keep.append(rp)
+        ins[t] = ctypes.cast(rp, ctypes.POINTER(c_u8_p))
+    out = np.zeros((nq, efs), np.uint8)
+    _lib.load().assemblDPFTreeQueryThreadResults(ctypes.byref(server.s), ins, T, _row_ptrs(out))
+    return out
+
+
+class Client:
+    """The synthetic-DB client of src/c/client.cpp:16-41 (server setup path)."""
+
+    def __init__(self, log_num_files, file_size_bytes):
+        self._lib = _lib.load()
+        self.c = CClient()
+        self._lib.initialize_client(ctypes.byref(self.c), log_num_files, file_size_bytes)
+
+    def encode_across_files_server(self, server):
+        self._lib.encode_across_files_server(ctypes.byref(self.c), ctypes.byref(server.s))
+
+    def free_client(self):
+        if self.c.unencoded_files:
+            self._lib.free_client(ctypes.byref(self.c))

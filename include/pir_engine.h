@@ -1,0 +1,119 @@
+/* pir_engine.h -- C ABI of the MI355X tree-DPF PIR answer engine (libpir_engine.so).
+ *
+ * Plain pointers and sizes only.  One engine = one PIR server's shard (or one partition of
+ * it) resident in the HBM of one GPU.  Every entry point returns 0 on success and a
+ * negative PIR_E* code on failure (message: pir_engine_last_error()); the server.h-compatible
+ * shim (pir_server.h) turns failures into abort(), like the reference's handleErrors()
+ * (src/c/utils.cpp:11-15).
+ *
+ * Reference interfaces replaced (paths relative to /root/reference/src/c):
+ *   pir_engine_create / _destroy     initializeServer / freeServer          server.cpp:17-52
+ *   pir_engine_set_shard[_rows]      the indexList rows written by encode_across_files_server
+ *                                                                           client.cpp:93-97
+ *   pir_engine_answer                runOptimizedDPFTreeQuery               server.cpp:96-134
+ *   pir_engine_answer_slice          runOptimizedDPFTreeQueryThread (intended semantics)
+ *                                                                           server.cpp:505-549
+ *   pir_engine_eval_all              evalAllOptimizedDPF                    dpf_tree.cpp:473-598
+ *   pir_engine_key_len               calcOptimizedDPFTreeKeyLength          utils.cpp:85-90
+ *   pir_comm_* + partitions          (new) split-shard across GPUs, XOR all-reduce over RCCL
+ */
+#ifndef PIR_ENGINE_H
+#define PIR_ENGINE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PIR_OK 0
+#define PIR_EINVAL (-1)  /* bad argument / unsupported shape          */
+#define PIR_EHIP (-2)    /* a HIP runtime call failed                  */
+#define PIR_ENOMEM (-3)  /* device or host allocation failed           */
+#define PIR_ECOMM (-4)   /* RCCL failure                               */
+#define PIR_ESTATE (-5)  /* call not valid in the engine's state       */
+
+#define PIR_MAX_PARTIES 17 /* p - 1 <= 16 control bits                   */
+#define PIR_MAX_ROUNDS 16  /* NUM_ROUNDS bytes come from one AES block   */
+#define PIR_MAX_LOG_RECORDS 40
+
+typedef struct pir_engine pir_engine_t;
+
+typedef struct {
+    int device;             /* HIP device ordinal                                     */
+    int num_parties;        /* p = NUM_PARTIES (2..17)                                */
+    int party_index;        /* 1-based, as server.partyIndex                          */
+    int log_num_records;    /* n = LOG_NUM_ENCODED_FILES: depth of the DPF tree       */
+    uint32_t record_bytes;  /* ENCODED_FILE_SIZE_BYTES                                */
+    int num_rounds;         /* NUM_ROUNDS (1..16): output bytes per leaf              */
+    int log_num_partitions; /* G: the logical shard is split into 2^G row partitions  */
+    int partition_index;    /* which partition this engine holds (0 when G == 0)      */
+    int is_byzantine;       /* answers are random bytes (server.cpp:116-119)          */
+} pir_engine_config;
+
+const char *pir_engine_last_error(void);
+int pir_engine_create(const pir_engine_config *cfg, pir_engine_t **out);
+void pir_engine_destroy(pir_engine_t *e);
+int pir_engine_key_len(int num_parties, int log_num_records, int num_rounds);
+/* records (rows) held by this engine = 2^(n - G) */
+uint64_t pir_engine_num_rows(const pir_engine_t *e);
+
+/* ---- shard (device-resident; rows are this engine's partition, row 0 = its first) ---- */
+/* rows [row0, row0+nrows) from a host buffer with src_pitch bytes between rows */
+int pir_engine_set_shard(pir_engine_t *e, const uint8_t *host, uint64_t row0, uint64_t nrows,
+                         uint64_t src_pitch);
+/* rows [row0, row0+nrows) from an array of row pointers (server.indexList) */
+int pir_engine_set_shard_rows(pir_engine_t *e, const uint8_t *const *rows, uint64_t row0,
+                              uint64_t nrows);
+/* synthetic shard generated on the device (bench): byte b of GLOBAL row i is a function of
+ * (seed, i, b), so every partition of a logical shard agrees with the whole */
+int pir_engine_fill_shard_random(pir_engine_t *e, uint64_t seed);
+int pir_engine_get_shard_row(pir_engine_t *e, uint64_t row, uint8_t *out);
+/* rows [row0, row0+nrows) back to the host, record_bytes per row, packed */
+int pir_engine_get_shard(pir_engine_t *e, uint64_t row0, uint64_t nrows, uint8_t *out);
+
+/* ---- answers, host buffers (synchronous; key_len bytes of key) ---- */
+/* result: num_rounds * record_bytes bytes, round a at result + a*record_bytes.  With a
+ * communicator attached (pir_comm_attach) every rank receives the XOR over partitions. */
+int pir_engine_answer(pir_engine_t *e, const uint8_t *key, uint8_t *result);
+/* partial answer over the engine rows [t*R/T, (t+1)*R/T), R = rows held, T a power of 2 */
+int pir_engine_answer_slice(pir_engine_t *e, const uint8_t *key, int thread_num,
+                            int num_threads, uint8_t *result);
+/* DPF shares of this engine's rows: out[a*R + i] (dataShare[a][i]) */
+int pir_engine_eval_all(pir_engine_t *e, const uint8_t *key, uint8_t *out);
+
+/* ---- answers, device-resident (asynchronous on `stream`, a hipStream_t or NULL for the
+ *      engine's own stream) ---- */
+int pir_engine_answer_dev(pir_engine_t *e, const uint8_t *d_key, uint8_t *d_result,
+                          void *stream);
+/* `num_keys` keys of key_len bytes back to back; results num_keys x num_rounds x record_bytes */
+int pir_engine_answer_batch_dev(pir_engine_t *e, const uint8_t *d_keys, int num_keys,
+                                uint8_t *d_result, void *stream);
+void *pir_engine_stream(pir_engine_t *e);
+int pir_engine_sync(pir_engine_t *e);
+/* device scratch the caller may use for keys/results (freed with the engine) */
+int pir_engine_alloc_dev(pir_engine_t *e, size_t bytes, void **d_ptr);
+int pir_engine_memcpy_h2d(pir_engine_t *e, void *d_dst, const void *h_src, size_t bytes);
+int pir_engine_memcpy_d2h(pir_engine_t *e, void *h_dst, const void *d_src, size_t bytes);
+
+/* ---- per-phase device time of answers (HIP events on the answering stream) ---- */
+/* phases: key_prep, tree_frontier, tree_leaves, scan, reduce, comm_fold.  `slots` event sets
+ * are kept in a ring (0 = off); last_timings averages the answers recorded since the previous
+ * read (at most `slots`), fills up to `max` {name, ms} pairs and returns the count. */
+typedef struct {
+    char name[32];
+    float ms;
+} pir_kernel_time;
+int pir_engine_set_profiling(pir_engine_t *e, int slots);
+int pir_engine_last_timings(pir_engine_t *e, pir_kernel_time *out, int max);
+
+/* ---- split shard across GPUs: XOR all-reduce of partition answers over RCCL ---- */
+#define PIR_COMM_ID_BYTES 128
+int pir_comm_unique_id(uint8_t id[PIR_COMM_ID_BYTES]);
+/* rank r of nranks; nranks must equal 2^G of the engine's config and r its partition */
+int pir_comm_attach(pir_engine_t *e, const uint8_t id[PIR_COMM_ID_BYTES], int nranks, int rank);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,218 @@
+// ref_driver.cpp -- TEST INFRASTRUCTURE ONLY (never shipped, never on the product path).
+//
+// A thin extern "C" harness around the reference's own C++ sources
+// (/root/reference/src/c/*.cpp, compiled where they lie by oracle/Makefile into
+// oracle/_ref/libref.so).  It exists for two purposes:
+//   1. generating the golden fixtures under tests/golden/ (tests/golden/make_golden.py);
+//   2. the "reference" CPU baseline leg of bench.py (runOptimizedDPFTreeQuery timed on the
+//      GPU box's host cores).
+// Nothing here re-implements the reference: every entry point calls the reference symbol
+// named in its comment.  No reference source is copied into this repository.
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <vector>
+
+#include "utils.h"
+#include "coding.h"
+#include "params.h"
+#include "dpf_tree.h"
+#include "server.h"
+#include "client.h"
+
+extern "C" {
+
+// utils.cpp:37-51
+void ref_G(const uint8_t* seed, uint32_t plen, uint8_t* out) {
+    EVP_CIPHER_CTX* ctx = EVP_CIPHER_CTX_new();
+    uint8_t s[16];
+    memcpy(s, seed, 16);
+    G(ctx, s, plen, out);
+    EVP_CIPHER_CTX_free(ctx);
+}
+
+// coding.cpp:9-60
+uint8_t ref_gf_mul(uint8_t a, uint8_t b) { return gf_mul(a, b); }
+uint8_t ref_gf_inv(uint8_t a) { return gf_inv(a); }
+uint8_t ref_gf_pow(uint8_t a, uint8_t e) { return gf_pow(a, e); }
+
+// utils.cpp:85-90
+int ref_key_len(int p, int n, int nq) { return calcOptimizedDPFTreeKeyLength(p, n, nq); }
+// utils.cpp:53-55
+uint32_t ref_blen(uint32_t p) { return blen(p); }
+
+// dpf_tree.cpp:142-274 (root seeds from RAND_bytes: the output keys ARE the fixture)
+void ref_gen_opt_dpf(int n, uint64_t index, const uint8_t* finalCW, int p, int nq,
+                     uint8_t* keys_out) {
+    EVP_CIPHER_CTX* ctx = EVP_CIPHER_CTX_new();
+    int kl = calcOptimizedDPFTreeKeyLength(p, n, nq);
+    std::vector<uint8_t> fcw(finalCW, finalCW + nq * (p - 1));
+    uint8_t** keys = (uint8_t**)malloc(p * sizeof(uint8_t*));
+    for (int j = 0; j < p; j++) keys[j] = (uint8_t*)malloc(kl);
+    genOptimizedDPF(ctx, n, (uint128_t)index, 1, fcw, p, nq, &keys);
+    for (int j = 0; j < p; j++) {
+        memcpy(keys_out + (size_t)j * kl, keys[j], kl);
+        free(keys[j]);
+    }
+    free(keys);
+    EVP_CIPHER_CTX_free(ctx);
+}
+
+// dpf_tree.cpp:473-598; out is nq x 2^n (a-major, like dataShare[a][j])
+void ref_eval_all_opt(int p, int party0, int n, const uint8_t* key, int nq, uint8_t* out) {
+    EVP_CIPHER_CTX* ctx = EVP_CIPHER_CTX_new();
+    size_t N = (size_t)1 << n;
+    uint8_t** ds = (uint8_t**)malloc(nq * sizeof(uint8_t*));
+    for (int a = 0; a < nq; a++) ds[a] = out + a * N;
+    evalAllOptimizedDPF(ctx, p, party0, n, (uint8_t*)key, 1, nq, ds);
+    free(ds);
+    EVP_CIPHER_CTX_free(ctx);
+}
+
+// dpf_tree.cpp:600-765 -- the DEFECTIVE threaded eval (negative fixture only)
+void ref_eval_all_opt_thread(int p, int party0, int n, const uint8_t* key, int nq,
+                             int threadNum, int numThreads, uint8_t* out) {
+    EVP_CIPHER_CTX* ctx = EVP_CIPHER_CTX_new();
+    size_t N = (size_t)1 << n;
+    uint8_t** ds = (uint8_t**)malloc(nq * sizeof(uint8_t*));
+    for (int a = 0; a < nq; a++) ds[a] = out + a * N;
+    evalAllOptimizedDPFThread(ctx, p, party0, n, (uint8_t*)key, 1, nq, ds, threadNum, numThreads);
+    free(ds);
+    EVP_CIPHER_CTX_free(ctx);
+}
+
+static void set_tree_globals(int p, int n, int efs, int nq) {
+    NUM_PARTIES = p;
+    LOG_NUM_ENCODED_FILES = n;
+    NUM_ENCODED_FILES = 1 << n;
+    ENCODED_FILE_SIZE_BYTES = efs;
+    NUM_ROUNDS = nq;
+    IS_HERMITE = 0;
+}
+
+// A resident reference server (server.cpp:17-42) holding a contiguous N x efs shard.
+struct ref_srv {
+    server s;
+    int p, n, efs, nq;
+};
+
+void* ref_server_new(int p, int party1, int n, int efs, int nq, const uint8_t* shard,
+                     int isByzantine, int numThreads) {
+    set_tree_globals(p, n, efs, nq);
+    ref_srv* h = new ref_srv;
+    h->p = p; h->n = n; h->efs = efs; h->nq = nq;
+    initializeServer(&h->s, party1, n, efs, isByzantine, numThreads);
+    size_t N = (size_t)1 << n;
+    for (size_t i = 0; i < N; i++) memcpy(h->s.indexList[i], shard + i * efs, efs);
+    return h;
+}
+
+// server.cpp:96-134; result is nq x efs
+void ref_server_answer(void* hv, const uint8_t* key, uint8_t* result) {
+    ref_srv* h = (ref_srv*)hv;
+    set_tree_globals(h->p, h->n, h->efs, h->nq);
+    uint8_t** res = (uint8_t**)malloc(h->nq * sizeof(uint8_t*));
+    for (int a = 0; a < h->nq; a++) res[a] = result + (size_t)a * h->efs;
+    runOptimizedDPFTreeQuery(&h->s, (uint8_t*)key, h->nq, res);
+    free(res);
+}
+
+// server.cpp:505-549 + :553-562 (defective thread path; negative fixture only)
+void ref_server_answer_threads(void* hv, const uint8_t* key, int numThreads, uint8_t* result) {
+    ref_srv* h = (ref_srv*)hv;
+    set_tree_globals(h->p, h->n, h->efs, h->nq);
+    uint8_t*** in = (uint8_t***)malloc(numThreads * sizeof(uint8_t**));
+    for (int t = 0; t < numThreads; t++) {
+        in[t] = (uint8_t**)malloc(h->nq * sizeof(uint8_t*));
+        for (int a = 0; a < h->nq; a++) in[t][a] = (uint8_t*)malloc(h->efs);
+        runOptimizedDPFTreeQueryThread(&h->s, (uint8_t*)key, t, numThreads, in[t]);
+    }
+    uint8_t** res = (uint8_t**)malloc(h->nq * sizeof(uint8_t*));
+    for (int a = 0; a < h->nq; a++) res[a] = result + (size_t)a * h->efs;
+    assemblDPFTreeQueryThreadResults(&h->s, in, numThreads, res);
+    for (int t = 0; t < numThreads; t++) {
+        for (int a = 0; a < h->nq; a++) free(in[t][a]);
+        free(in[t]);
+    }
+    free(in);
+    free(res);
+}
+
+void ref_server_free(void* hv) {
+    ref_srv* h = (ref_srv*)hv;
+    set_tree_globals(h->p, h->n, h->efs, h->nq);
+    freeServer(&h->s);
+    delete h;
+}
+
+// Wall-clock seconds of `reps` runOptimizedDPFTreeQuery calls (CPU-baseline leg).
+double ref_server_time(void* hv, const uint8_t* key, uint8_t* result, int reps) {
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int r = 0; r < reps; r++) ref_server_answer(hv, key, result);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}
+
+// params.cpp:467-642 sizing for tree mode: setSystemParams(L,f,t=1,k,r,b=0,rho,mac,mode=0)
+void ref_e2e_sizes(int L, int f, int k, int r, int rho, int* out5) {
+    setSystemParams(L, f, 1, k, r, 0, rho, 0, 0);
+    out5[0] = NUM_PARTIES;
+    out5[1] = LOG_NUM_ENCODED_FILES;
+    out5[2] = ENCODED_FILE_SIZE_BYTES;
+    out5[3] = NUM_ROUNDS;
+    out5[4] = calcOptimizedDPFTreeKeyLength(NUM_PARTIES, LOG_NUM_ENCODED_FILES, NUM_ROUNDS);
+}
+
+// The in-process cluster of correctness_tests.cpp:230-372 with the Go server's
+// encode-across setup (server.go:299-331): synthetic DB (client.cpp:16-33), p servers
+// encoded across files (client.cpp:70-97), keys (client.cpp:144-153), every party's
+// runOptimizedDPFTreeQuery answer, first r parties erased, decode (client.cpp:211-268).
+// Buffers: files[2^L*f], shards[p*N*efs], keys[p*kl], answers[p*nq*efs], decoded[f].
+// Returns 1 when decoded == file[idx].
+int ref_e2e(int L, int f, int k, int r, int rho, int idx, uint8_t* files, uint8_t* shards,
+            uint8_t* keys_out, uint8_t* answers, uint8_t* decoded) {
+    setSystemParams(L, f, 1, k, r, 0, rho, 0, 0);
+    int p = NUM_PARTIES, nq = NUM_ROUNDS, efs = ENCODED_FILE_SIZE_BYTES;
+    size_t N = NUM_ENCODED_FILES;
+    int kl = calcOptimizedDPFTreeKeyLength(p, LOG_NUM_ENCODED_FILES, nq);
+    client c;
+    initialize_client(&c, L, FILE_SIZE_BYTES);
+    for (int i = 0; i < NUM_FILES; i++) memcpy(files + (size_t)i * f, c.unencoded_files[i], f);
+    std::vector<server> servers(p);
+    for (int i = 0; i < p; i++) {
+        initializeServer(&servers[i], i + 1, LOG_NUM_ENCODED_FILES, efs, 0, 1);
+        encode_across_files_server(&c, &servers[i]);
+        for (size_t j = 0; j < N; j++)
+            memcpy(shards + ((size_t)i * N + j) * efs, servers[i].indexList[j], efs);
+    }
+    uint8_t** keys = (uint8_t**)malloc(p * sizeof(uint8_t*));
+    for (int j = 0; j < p; j++) keys[j] = (uint8_t*)malloc(kl);
+    generate_opt_DPF_tree_query(&c, idx, &keys);
+    std::vector<std::vector<uint8_t*>> resp(p, std::vector<uint8_t*>(nq));
+    for (int i = 0; i < p; i++) {
+        memcpy(keys_out + (size_t)i * kl, keys[i], kl);
+        for (int a = 0; a < nq; a++) resp[i][a] = answers + ((size_t)i * nq + a) * efs;
+        runOptimizedDPFTreeQuery(&servers[i], keys[i], nq, resp[i].data());
+    }
+    std::vector<uint8_t> erasure(p);
+    for (int i = 0; i < p; i++) erasure[i] = (i < r) ? 0 : 1;
+    int numResponses = p - r;
+    uint8_t*** test = (uint8_t***)malloc(numResponses * sizeof(uint8_t**));
+    for (int i = 0, cur = 0; i < p; i++) {
+        if (!erasure[i]) continue;
+        test[cur++] = resp[i].data();
+    }
+    std::vector<uint8_t> out(FILE_SIZE_BYTES);
+    assembleDPFTreeQueryResponses(&c, erasure.data(), test, out.data());
+    memcpy(decoded, out.data(), f);
+    int ok = memcmp(out.data(), c.unencoded_files[idx], f) == 0;
+    free(test);
+    for (int j = 0; j < p; j++) free(keys[j]);
+    free(keys);
+    for (int i = 0; i < p; i++) freeServer(&servers[i]);
+    return ok;
+}
+
+}  // extern "C"

@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/*.json from the REFERENCE itself.
+
+Test infrastructure only.  Requires oracle/_ref/libref.so, i.e. the reference's own
+src/c compiled from /root/reference by `make -C oracle ref` (this container only; the
+reference never travels to the GPU box -- these JSON files do).  Every expected output
+below is produced by a reference symbol (see oracle/ref_driver.cpp); the only thing this
+script computes itself is the synthetic shard INPUT (xorshift64, whose SHA-256 is stored so
+a different generator is caught).
+
+Root seeds come from the reference's RAND_bytes, so each fixture stores the full key bytes.
+
+    python tests/golden/make_golden.py     # rewrites tests/golden/*.json
+"""
+import ctypes
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libref.so"))
+U64 = ctypes.c_uint64
+SHARD_SEED = 0x9E3779B97F4A7C15
+
+
+def ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def xorshift_bytes(seed, n):
+    # x ^= x << 13; x ^= x >> 7; x ^= x << 17 (64-bit), output low byte per step
+    out = np.empty(n, np.uint8)
+    x = seed & 0xFFFFFFFFFFFFFFFF
+    M = 0xFFFFFFFFFFFFFFFF
+    for i in range(n):
+        x ^= (x << 13) & M
+        x ^= x >> 7
+        x ^= (x << 17) & M
+        out[i] = x & 0xFF
+    return out
+
+
+def final_cw(p, nq, rho, k):
+    # client.cpp:144-153 (computed through the reference's gf_pow)
+    out = []
+    for i in range(1, nq + 1):
+        for j in range(2, p + 1):
+            out.append(REF.ref_gf_pow(j, rho * i) ^ 1)
+    return np.array(out, np.uint8)
+
+
+def write(name, obj):
+    with open(os.path.join(HERE, name), "w") as f:
+        json.dump(obj, f, indent=1, sort_keys=True)
+    print("wrote", name)
+
+
+def prg_kats():
+    cases = []
+    rng = np.random.RandomState(1)
+    seeds = [bytes(range(16)), bytes(16), bytes(rng.randint(0, 256, 16, dtype=np.uint8))]
+    for s in seeds:
+        for plen in (16, 33, 34, 48):
+            out = np.zeros(plen, np.uint8)
+            REF.ref_G(s, plen, ptr(out))
+            cases.append({"seed": s.hex(), "plen": plen, "out": out.tobytes().hex()})
+    blen = {p: REF.ref_blen(p) for p in range(2, 18)}
+    keylen = {f"{p},{n},{nq}": REF.ref_key_len(p, n, nq)
+              for (p, n, nq) in [(2, 16, 1), (2, 20, 1), (2, 24, 1), (2, 27, 1), (8, 24, 5),
+                                 (3, 10, 1), (5, 12, 4), (8, 12, 5), (9, 10, 1)]}
+    write("prg_kat.json", {"G": cases, "blen": blen, "key_len": keylen})
+
+
+def gf_kats():
+    mul = np.array([[REF.ref_gf_mul(a, b) for b in range(256)] for a in range(256)], np.uint8)
+    pw = np.array([[REF.ref_gf_pow(a, e) for e in range(256)] for a in range(256)], np.uint8)
+    inv = np.array([REF.ref_gf_inv(a) for a in range(256)], np.uint8)
+    spot = {"02*80": int(mul[2, 0x80]), "53*ca": int(mul[0x53, 0xCA]), "ff*ff": int(mul[255, 255]),
+            "inv02": int(inv[2]), "pow(2,8)": int(pw[2, 8]), "pow(0,5)": int(pw[0, 5])}
+    write("gf_kat.json", {"mul_sha256": sha(mul), "pow_sha256": sha(pw), "inv": inv.tobytes().hex(),
+                          "spot": spot})
+
+
+def dpf_and_answers():
+    cases = []
+    for (p, n, nq, idx) in [(2, 10, 1, 77), (3, 10, 1, 513), (5, 12, 4, 4000), (8, 12, 5, 1234),
+                            (9, 10, 1, 1023), (2, 16, 1, 21845)]:
+        kl = REF.ref_key_len(p, n, nq)
+        fcw = final_cw(p, nq, 1, nq)
+        keys = np.zeros(p * kl, np.uint8)
+        REF.ref_gen_opt_dpf(n, U64(idx), ptr(fcw), p, nq, ptr(keys))
+        N = 1 << n
+        parties = []
+        for party in range(p):
+            c = np.zeros(nq * N, np.uint8)
+            REF.ref_eval_all_opt(p, party, n, ptr(keys[party * kl:]), nq, ptr(c))
+            ent = {"key": keys[party * kl:(party + 1) * kl].tobytes().hex(), "c_sha256": sha(c)}
+            if n <= 10:
+                ent["c"] = c.tobytes().hex()
+            parties.append(ent)
+        answers = {}
+        for efs in ((8, 256) if n <= 12 else (256,)):
+            shard = xorshift_bytes(SHARD_SEED, N * efs)
+            per = []
+            for party in range(p):
+                h = REF.ref_server_new(p, party + 1, n, efs, nq, ptr(shard), 0, 1)
+                res = np.zeros(nq * efs, np.uint8)
+                REF.ref_server_answer(ctypes.c_void_p(h), ptr(keys[party * kl:]), ptr(res))
+                REF.ref_server_free(ctypes.c_void_p(h))
+                per.append(res.tobytes().hex())
+            answers[str(efs)] = {"shard_sha256": sha(shard), "answers": per}
+        cases.append({"p": p, "n": n, "nq": nq, "index": idx, "final_cw": fcw.tobytes().hex(),
+                      "key_len": kl, "parties": parties, "answers": answers})
+        print("dpf case", p, n, nq)
+    write("dpf_eval.json", {"shard_seed": SHARD_SEED, "cases": cases})
+
+
+def e2e():
+    restype = ctypes.c_int
+    REF.ref_e2e.restype = restype
+    cases = []
+    for (L, f, k, r, idx) in [(10, 8, 1, 1, 5), (10, 8, 2, 1, 300), (12, 16, 4, 2, 77),
+                              (12, 16, 5, 2, 501), (11, 32, 3, 1, 100)]:
+        rho = 1
+        s = (ctypes.c_int * 5)()
+        REF.ref_e2e_sizes(L, f, k, r, rho, s)
+        p, n, efs, nq, kl = list(s)
+        N = 1 << n
+        files = np.zeros((1 << L) * f, np.uint8)
+        shards = np.zeros(p * N * efs, np.uint8)
+        keys = np.zeros(p * kl, np.uint8)
+        ans = np.zeros(p * nq * efs, np.uint8)
+        dec = np.zeros(f, np.uint8)
+        ok = REF.ref_e2e(L, f, k, r, rho, idx, ptr(files), ptr(shards), ptr(keys), ptr(ans), ptr(dec))
+        assert ok == 1, (L, f, k, r)
+        cases.append({
+            "L": L, "f": f, "k": k, "r": r, "rho": rho, "index": idx,
+            "p": p, "n": n, "efs": efs, "nq": nq, "key_len": kl,
+            "files_sha256": sha(files),
+            "shard_sha256": [sha(shards[i * N * efs:(i + 1) * N * efs]) for i in range(p)],
+            "keys": [keys[i * kl:(i + 1) * kl].tobytes().hex() for i in range(p)],
+            "answers": [ans[i * nq * efs:(i + 1) * nq * efs].tobytes().hex() for i in range(p)],
+            "erasure": [0 if i < r else 1 for i in range(p)],
+            "decoded": dec.tobytes().hex(),
+        })
+        print("e2e case", L, f, k, r, "p", p, "nq", nq)
+    write("e2e.json", {"cases": cases})
+
+
+def thread_defect():
+    # server.cpp:505-562 as shipped: documents the defect; NOT a parity target.
+    p, n, nq, efs, T = 2, 10, 1, 8, 4
+    kl = REF.ref_key_len(p, n, nq)
+    fcw = final_cw(p, nq, 1, nq)
+    keys = np.zeros(p * kl, np.uint8)
+    REF.ref_gen_opt_dpf(n, U64(333), ptr(fcw), p, nq, ptr(keys))
+    shard = xorshift_bytes(SHARD_SEED, (1 << n) * efs)
+    h = REF.ref_server_new(p, 1, n, efs, nq, ptr(shard), 0, T)
+    good = np.zeros(nq * efs, np.uint8)
+    bad = np.zeros(nq * efs, np.uint8)
+    REF.ref_server_answer(ctypes.c_void_p(h), ptr(keys), ptr(good))
+    REF.ref_server_answer_threads(ctypes.c_void_p(h), ptr(keys), T, ptr(bad))
+    REF.ref_server_free(ctypes.c_void_p(h))
+    c_thr = np.zeros(nq * (1 << n), np.uint8)
+    REF.ref_eval_all_opt_thread(p, 0, n, ptr(keys), nq, 0, T, ptr(c_thr))
+    write("thread_defect.json", {"p": p, "n": n, "nq": nq, "efs": efs, "threads": T,
+                                 "key": keys[:kl].tobytes().hex(), "shard_sha256": sha(shard),
+                                 "answer_single": good.tobytes().hex(),
+                                 "answer_thread_assembled": bad.tobytes().hex(),
+                                 "thread0_c_nonzero": int((c_thr != 0).sum())})
+
+
+if __name__ == "__main__":
+    REF.ref_server_new.restype = ctypes.c_void_p
+    REF.ref_blen.restype = ctypes.c_uint32
+    for fn in (REF.ref_gf_mul, REF.ref_gf_pow, REF.ref_gf_inv):
+        fn.restype = ctypes.c_uint8
+    what = sys.argv[1:] or ["prg", "gf", "dpf", "e2e", "thread"]
+    if "prg" in what: prg_kats()
+    if "gf" in what: gf_kats()
+    if "dpf" in what: dpf_and_answers()
+    if "e2e" in what: e2e()
+    if "thread" in what: thread_defect()

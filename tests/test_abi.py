@@ -1,0 +1,87 @@
+"""The C-ABI library: loads without a GPU, exports every function include/*.h declares, and its
+pure-host pieces (sizing globals, key lengths, finalCW) agree with the reference fixtures.
+No GPU compute is called here."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from erasurecodedpir_amd import _lib
+
+INCLUDE = os.path.join(O.ROOT, "include")
+
+
+def declared_functions():
+    names = set()
+    for h in sorted(os.listdir(INCLUDE)):
+        if not h.endswith(".h"):
+            continue
+        src = open(os.path.join(INCLUDE, h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"//[^\n]*", "", src)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\([^;{]*\)\s*;", src, re.M):
+            if not m.group(0).lstrip().startswith(("typedef", "#", "return")):
+                names.add(m.group(1))
+    return names
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    lib = _lib.load()
+    names = declared_functions()
+    assert {"pir_engine_create", "pir_engine_answer", "runOptimizedDPFTreeQuery",
+            "runOptimizedDPFTreeQueryThread", "assemblDPFTreeQueryThreadResults",
+            "pir_gen_keys"} <= names
+    missing = [n for n in sorted(names) if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the ctypes prototypes cover exactly the declared surface
+    assert names == set(_lib.PROTOTYPES)
+
+
+def test_globals_exported():
+    for g in _lib.GLOBALS_INT + _lib.GLOBALS_U32:
+        _lib.global_int(g)
+
+
+def test_key_len_matches_reference():
+    g = O.golden("prg_kat.json")
+    from erasurecodedpir_amd import key_len
+    from erasurecodedpir_amd.server import calcOptimizedDPFTreeKeyLength
+    for k, kl in g["key_len"].items():
+        p, n, nq = map(int, k.split(","))
+        assert key_len(p, n, nq) == kl
+        assert calcOptimizedDPFTreeKeyLength(p, n, nq) == kl
+
+
+@pytest.mark.parametrize("ci", range(5))
+def test_setSystemParams_sizing_matches_reference(ci):
+    from erasurecodedpir_amd import server
+    case = O.golden("e2e.json")["cases"][ci]
+    server.setSystemParams(case["L"], case["f"], 1, case["k"], case["r"], 0, case["rho"], 0, 0)
+    prm = server.params()
+    assert prm["NUM_PARTIES"] == case["p"]
+    assert prm["LOG_NUM_ENCODED_FILES"] == case["n"]
+    assert prm["ENCODED_FILE_SIZE_BYTES"] == case["efs"]
+    assert prm["NUM_ROUNDS"] == case["nq"]
+    assert prm["NUM_ENCODED_FILES"] == 1 << case["n"]
+    assert prm["NUM_RESPONSES"] == case["p"] - case["r"]
+
+
+def test_final_cw_matches_reference():
+    from erasurecodedpir_amd.client import final_cw
+    for case in O.golden("dpf_eval.json")["cases"]:
+        p, nq = case["p"], case["nq"]
+        assert final_cw(p, nq, 1).tobytes().hex() == case["final_cw"]
+    for p, nq, rho in [(8, 5, 1), (17, 16, 1), (6, 2, 2), (9, 3, 3)]:
+        assert np.array_equal(final_cw(p, nq, rho), O.final_cw(p, nq, rho))
+
+
+def test_errors_are_loud_without_a_gpu():
+    """On a host without a usable device the engine refuses (no silent CPU path)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from erasurecodedpir_amd import Engine, PirError
+    with pytest.raises(PirError):
+        Engine(2, 1, 10, 16, 1)
