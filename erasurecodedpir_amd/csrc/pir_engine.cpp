@@ -62,6 +62,16 @@ struct DevBuf {
 
 }  // namespace
 
+// Event layout of one profiled answer.  Leaves and scans run as kMaxChunks-way pipelined
+// chunks on two streams (tree leaves of chunk j+1 overlap the shard scan of chunk j).
+constexpr int kMaxChunks = 8;
+enum {
+  EV_START = 0, EV_KEY = 1, EV_FRONT = 2,
+  EV_LEAF_B = 3, EV_LEAF_E = EV_LEAF_B + kMaxChunks,
+  EV_SCAN_B = EV_LEAF_E + kMaxChunks, EV_SCAN_E = EV_SCAN_B + kMaxChunks,
+  EV_PRERED = EV_SCAN_E + kMaxChunks, EV_RED, EV_END, kNumEv
+};
+
 struct pir_engine {
   pir_engine_config cfg{};
   int nrp = 1;
@@ -70,6 +80,10 @@ struct pir_engine {
   int key_len = 0;
   int num_cus = 256;
   hipStream_t stream = nullptr;
+  hipStream_t aux = nullptr;              // scan stream of the leaves/scan pipeline
+  hipEvent_t ev_leaf[kMaxChunks] = {};    // leaves of chunk j written
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int last_chunks = 1;
   uint8_t* d_shard = nullptr;
   uint8_t* d_key_raw = nullptr;  // max_batch keys
   pir::DevKey* d_keys = nullptr; // max_batch parsed keys
@@ -89,7 +103,7 @@ struct pir_engine {
   uint64_t byz_counter = 0;
   // profiling: a ring of event sets, one per answer, read back after a sync
   struct ProfSlot {
-    hipEvent_t ev[7];
+    hipEvent_t ev[kNumEv];
   };
   std::vector<ProfSlot> prof;
   int prof_next = 0, prof_count = 0;
@@ -122,49 +136,88 @@ int ensure_slabs(pir_engine* e, size_t bytes) {
   return PIR_OK;
 }
 
+int pick_chunks(const pir::TreePlan& pl) {
+  // pipeline only when every chunk still fills the GPU (>= 2^16 records)
+  int c = 1;
+  while (c < kMaxChunks && (pl.nfront / pl.tile) % (2 * c) == 0 && (pl.nleaves >> 16) >= (uint64_t)(2 * c))
+    c *= 2;
+  return c;
+}
+
 // Answer one partition slice: rows [row0, row0 + 2^(n - log_parts_total)) of this engine
 // with the tree rooted at `prefix` (depth log_parts_total).  d_key points at ONE parsed key.
+//   s  : key prep, frontier, leaves(0..C-1), [join], reduce
+//   aux: scan(j) after leaves(j)  -- so leaves(j+1) overlaps scan(j)
 int answer_core(pir_engine* e, const pir::DevKey* d_key, int log_parts_total, uint64_t prefix,
                 uint64_t row0, uint8_t* d_out, hipStream_t s) {
   const auto& c = e->cfg;
   const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix);
-  const uint64_t nrec = pl.nleaves;
+  const int C = pick_chunks(pl);
+  e->last_chunks = C;
+  const uint64_t nrec = pl.nleaves / C, nfc = pl.nfront / C;
   const pir::ScanShape sh = pir::make_scan_shape(nrec, e->pitch, c.num_rounds, e->num_cus);
   int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
   if (rc) return rc;
   hipEvent_t* ev = e->ev;
-  if (ev) HIP_TRY(hipEventRecord(ev[1], s));
-  HIP_TRY(pir::launch_tree(pl, d_key, e->d_front_s, e->d_front_t, e->d_c, e->nrp, s,
-                           ev ? ev[2] : nullptr));
-  if (ev) HIP_TRY(hipEventRecord(ev[3], s));
-  HIP_TRY(pir::launch_scan(sh, e->d_shard + row0 * e->pitch, nrec, e->d_c, e->d_slabs, s));
-  if (ev) HIP_TRY(hipEventRecord(ev[4], s));
+  if (ev) HIP_TRY(hipEventRecord(ev[EV_KEY], s));
+  HIP_TRY(pir::launch_frontier(pl, d_key, e->d_front_s, e->d_front_t, s));
+  if (ev) HIP_TRY(hipEventRecord(ev[EV_FRONT], s));
+  for (int j = 0; j < C; ++j) {
+    if (ev) HIP_TRY(hipEventRecord(ev[EV_LEAF_B + j], s));
+    HIP_TRY(pir::launch_leaves(pl, d_key, e->d_front_s, e->d_front_t, j * nfc, nfc, e->d_c,
+                               e->nrp, s));
+    if (ev) HIP_TRY(hipEventRecord(ev[EV_LEAF_E + j], s));
+    HIP_TRY(hipEventRecord(e->ev_leaf[j], s));
+    HIP_TRY(hipStreamWaitEvent(e->aux, e->ev_leaf[j], 0));
+    if (ev) HIP_TRY(hipEventRecord(ev[EV_SCAN_B + j], e->aux));
+    HIP_TRY(pir::launch_scan(sh, e->d_shard + (row0 + j * nrec) * e->pitch, nrec,
+                             e->d_c + j * nrec * e->nrp, e->d_slabs, j > 0, e->aux));
+    if (ev) HIP_TRY(hipEventRecord(ev[EV_SCAN_E + j], e->aux));
+  }
+  HIP_TRY(hipEventRecord(e->ev_join, e->aux));
+  HIP_TRY(hipStreamWaitEvent(s, e->ev_join, 0));
+  if (ev) HIP_TRY(hipEventRecord(ev[EV_PRERED], s));
   HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, d_out, s));
-  if (ev) HIP_TRY(hipEventRecord(ev[5], s));
+  if (ev) HIP_TRY(hipEventRecord(ev[EV_RED], s));
   return PIR_OK;
 }
 
 int check_key_ptr(const void* p) { return p ? PIR_OK : fail(PIR_EINVAL, "null key"); }
 
-const char* const kPhaseNames[6] = {"key_prep", "tree_frontier", "tree_leaves",
-                                    "scan", "reduce", "comm_fold"};
+const char* const kPhaseNames[] = {"key_prep", "tree_frontier", "tree_leaves", "scan",
+                                   "reduce", "comm_fold", "total", "chunks"};
+constexpr int kNumPhases = 8;
 
-// Average per-phase times over the answers recorded since the last read.
+// Mean per-phase device times over the answers recorded since the last read.  tree_leaves and
+// scan are the summed kernel durations of the C pipelined chunks (they overlap each other).
 int read_timings(pir_engine* e, pir_kernel_time* out, int max) {
-  const int n = std::min(max, 6);
+  const int n = std::min(max, kNumPhases);
   if (e->prof.empty() || e->prof_count == 0) return 0;
-  const int cnt = e->prof_count, sz = (int)e->prof.size();
-  HIP_TRY(hipEventSynchronize(e->prof[(e->prof_next + sz - 1) % sz].ev[6]));
-  for (int i = 0; i < n; ++i) {
-    double acc = 0;
-    for (int k = 0; k < cnt; ++k) {
-      const auto& sl = e->prof[(e->prof_next + sz - cnt + k) % sz];
-      float ms = 0;
-      HIP_TRY(hipEventElapsedTime(&ms, sl.ev[i], sl.ev[i + 1]));
-      acc += ms;
+  const int cnt = e->prof_count, sz = (int)e->prof.size(), C = e->last_chunks;
+  HIP_TRY(hipEventSynchronize(e->prof[(e->prof_next + sz - 1) % sz].ev[EV_END]));
+  double acc[kNumPhases] = {};
+  auto el = [](hipEvent_t a, hipEvent_t b, double& sum) -> hipError_t {
+    float ms = 0;
+    hipError_t r = hipEventElapsedTime(&ms, a, b);
+    sum += ms;
+    return r;
+  };
+  for (int k = 0; k < cnt; ++k) {
+    const hipEvent_t* v = e->prof[(e->prof_next + sz - cnt + k) % sz].ev;
+    HIP_TRY(el(v[EV_START], v[EV_KEY], acc[0]));
+    HIP_TRY(el(v[EV_KEY], v[EV_FRONT], acc[1]));
+    for (int j = 0; j < C; ++j) {
+      HIP_TRY(el(v[EV_LEAF_B + j], v[EV_LEAF_E + j], acc[2]));
+      HIP_TRY(el(v[EV_SCAN_B + j], v[EV_SCAN_E + j], acc[3]));
     }
+    HIP_TRY(el(v[EV_PRERED], v[EV_RED], acc[4]));
+    HIP_TRY(el(v[EV_RED], v[EV_END], acc[5]));
+    HIP_TRY(el(v[EV_START], v[EV_END], acc[6]));
+  }
+  acc[7] = C * cnt;
+  for (int i = 0; i < n; ++i) {
     snprintf(out[i].name, sizeof out[i].name, "%s", kPhaseNames[i]);
-    out[i].ms = (float)(acc / cnt);
+    out[i].ms = (float)(acc[i] / cnt);
   }
   e->prof_count = 0;
   return n;
@@ -180,11 +233,13 @@ int answer_dev_locked(pir_engine* e, const uint8_t* d_key, uint8_t* d_result, hi
     e->prof_count = std::min(e->prof_count + 1, (int)e->prof.size());
   }
   hipEvent_t* ev = e->ev;
-  if (ev) HIP_TRY(hipEventRecord(ev[0], s));
+  if (ev) HIP_TRY(hipEventRecord(ev[EV_START], s));
   if (c.is_byzantine) {  // server.cpp:116-119: random answer bytes
     HIP_TRY(pir::launch_fill_random(d_result, out_bytes, 0xB42u + (++e->byz_counter), s));
     if (ev)
-      for (int i = 1; i < 7; ++i) HIP_TRY(hipEventRecord(ev[i], s));
+      for (int i = 1; i < kNumEv; ++i) HIP_TRY(hipEventRecord(ev[i], s));
+    e->last_chunks = 1;
+    e->ev = nullptr;
     return PIR_OK;
   }
   HIP_TRY(pir::launch_key_prep(d_key, e->key_len, 1, c.num_parties, c.log_num_records,
@@ -197,7 +252,7 @@ int answer_dev_locked(pir_engine* e, const uint8_t* d_key, uint8_t* d_result, hi
     RCCL_TRY(ncclAllGather(e->d_part, e->d_gather, out_bytes, ncclUint8, e->comm, s));
     HIP_TRY(pir::launch_xor_fold(e->d_gather, e->nranks, out_bytes, d_result, s));
   }
-  if (ev) HIP_TRY(hipEventRecord(ev[6], s));
+  if (ev) HIP_TRY(hipEventRecord(ev[EV_END], s));
   e->ev = nullptr;
   return PIR_OK;
 }
@@ -241,8 +296,15 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
   auto cleanup = [&](int rc) { pir_engine_destroy(e); return rc; };
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, c.device) == hipSuccess) e->num_cus = prop.multiProcessorCount;
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail(PIR_EHIP, "hipStreamCreate failed"));
+  for (auto& ev : e->ev_leaf)
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+      return cleanup(fail(PIR_EHIP, "hipEventCreate failed"));
+  if (hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess)
+    return cleanup(fail(PIR_EHIP, "hipEventCreate failed"));
   pir::upload_aes_table(e->stream);
   const size_t shard_bytes = (size_t)e->rows * e->pitch;
   if (hipMalloc(&e->d_shard, shard_bytes) != hipSuccess)
@@ -270,6 +332,7 @@ void pir_engine_destroy(pir_engine_t* e) {
   if (!e) return;
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->aux) (void)hipStreamSynchronize(e->aux);
   if (e->comm) (void)ncclCommDestroy(e->comm);
   for (auto* p : {(void*)e->d_shard, (void*)e->d_key_raw, (void*)e->d_keys, (void*)e->d_front_s,
                   (void*)e->d_front_t, (void*)e->d_c, (void*)e->d_slabs, (void*)e->d_part,
@@ -280,6 +343,11 @@ void pir_engine_destroy(pir_engine_t* e) {
   if (e->h_res) (void)hipHostFree(e->h_res);
   for (auto& sl : e->prof)
     for (auto& ev : sl.ev) (void)hipEventDestroy(ev);
+  for (auto& ev : e->ev_leaf)
+    if (ev) (void)hipEventDestroy(ev);
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+  if (e->aux) (void)hipStreamDestroy(e->aux);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }

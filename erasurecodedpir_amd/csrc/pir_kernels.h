@@ -10,7 +10,9 @@ constexpr int kMaxLevels = 40;  // PIR_MAX_LOG_RECORDS
 constexpr int kMaxCW = 16;      // p - 1 <= 16
 constexpr int kNodeCap = 1024;  // tree nodes per LDS level buffer
 constexpr int kTreeThreads = 512;
-constexpr int kScanThreads = 256;
+constexpr int kScanThreads = 512;
+constexpr int kScanBlocksPerCU = 2;
+constexpr int kReduceThreads = 1024;
 constexpr int kColGroupLanes = 64;  // one wave's lanes cover a column group of a record
 
 // One DPF key, parsed for the device (written by k_key_prep from the raw key bytes whose
@@ -43,9 +45,18 @@ void upload_aes_table(hipStream_t s);  // Te0 (computed on the host) -> __consta
 
 hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys, int p, int n,
                            int nq, int party0, DevKey* d_keys, hipStream_t s);
-hipError_t launch_tree(const TreePlan& pl, const DevKey* d_key, uint4* d_front_s,
-                       uint32_t* d_front_t, uint8_t* d_c, int nrp, hipStream_t s,
-                       hipEvent_t mid = nullptr);
+hipError_t launch_frontier(const TreePlan& pl, const DevKey* d_key, uint4* d_front_s,
+                           uint32_t* d_front_t, hipStream_t s);
+// leaves of frontier nodes [f0, f0 + nf) (nf a multiple of pl.tile) -> c rows [f0<<d, ...)
+hipError_t launch_leaves(const TreePlan& pl, const DevKey* d_key, const uint4* d_front_s,
+                         const uint32_t* d_front_t, uint64_t f0, uint64_t nf, uint8_t* d_c,
+                         int nrp, hipStream_t s);
+inline hipError_t launch_tree(const TreePlan& pl, const DevKey* d_key, uint4* d_front_s,
+                              uint32_t* d_front_t, uint8_t* d_c, int nrp, hipStream_t s) {
+  hipError_t e = launch_frontier(pl, d_key, d_front_s, d_front_t, s);
+  if (e != hipSuccess) return e;
+  return launch_leaves(pl, d_key, d_front_s, d_front_t, 0, pl.nfront, d_c, nrp, s);
+}
 // scan rows [0, nrec) of `shard` (row pitch `pitch`) with coefficients cT[i*nrp + a]
 struct ScanShape {
   int nq, nrp, vec;      // vec = dwords per lane chunk (4, 2, 1)
@@ -55,8 +66,9 @@ struct ScanShape {
   dim3 grid;
 };
 ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus);
+// accumulate: XOR into the slabs instead of overwriting them (chunked scans of one answer)
 hipError_t launch_scan(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
-                       const uint8_t* d_c, uint8_t* d_slabs, hipStream_t s);
+                       const uint8_t* d_c, uint8_t* d_slabs, bool accumulate, hipStream_t s);
 // XOR the slabs, compact pitch -> record_bytes: d_out[a*efs + b]
 hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t efs,
                          uint8_t* d_out, hipStream_t s);

@@ -279,7 +279,7 @@ template <int NQ, int NRP, int VEC, bool UNI>
 __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict__ shard,
                                                        uint64_t nrec, uint32_t pitch,
                                                        uint32_t cpr, const uint8_t* __restrict__ c,
-                                                       uint8_t* __restrict__ slabs) {
+                                                       uint8_t* __restrict__ slabs, int accumulate) {
   constexpr int CH = VEC * 4;  // bytes per lane chunk
   constexpr int GW = kColGroupLanes * VEC;  // words per column group
   __shared__ uint32_t red[NQ * GW];
@@ -381,20 +381,44 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
   __syncthreads();
   uint32_t* slab = reinterpret_cast<uint32_t*>(slabs) +
                    ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * (NQ * GW);
-  for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) slab[i] = red[i];
+  if (accumulate)
+    for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) slab[i] ^= red[i];
+  else
+    for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) slab[i] = red[i];
 }
 
-// slabs: [grid.y][grid.x][nq][GW words]; out[a*efs + b] for b < efs
-__global__ void k_reduce(const uint32_t* __restrict__ slabs, int nq, uint32_t gw, uint32_t gx,
-                         uint32_t gy, uint32_t pitch, uint32_t efs, uint8_t* __restrict__ out) {
+// slabs: [grid.y][grid.x][nq][GW words]; out[a*efs + b] for b < efs.
+// One 1024-thread block per 64 output words: 16 lane groups split the gx slabs, then LDS.
+__global__ __launch_bounds__(kReduceThreads) void k_reduce(const uint32_t* __restrict__ slabs,
+                                                           int nq, uint32_t gw, uint32_t gx,
+                                                           uint32_t pitch, uint32_t efs,
+                                                           uint8_t* __restrict__ out) {
+  __shared__ uint32_t part[kReduceThreads / 64][64];
   const uint32_t words = pitch / 4;
-  const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (uint32_t)nq * words) return;
-  const uint32_t a = idx / words, w = idx - a * words;
-  const uint32_t grp = w / gw, win = w - grp * gw;
-  const uint32_t* p = slabs + ((uint64_t)grp * gx) * nq * gw + (uint64_t)a * gw + win;
+  const uint32_t lane = threadIdx.x & 63, grp16 = threadIdx.x >> 6, ngrp = blockDim.x >> 6;
+  const uint32_t idx = blockIdx.x * 64 + lane;
   uint32_t acc = 0;
-  for (uint32_t x = 0; x < gx; ++x) acc ^= p[(uint64_t)x * nq * gw];
+  if (idx < (uint32_t)nq * words) {
+    const uint32_t a = idx / words, w = idx - a * words;
+    const uint32_t grp = w / gw, win = w - grp * gw;
+    const uint32_t* p = slabs + ((uint64_t)grp * gx) * nq * gw + (uint64_t)a * gw + win;
+    const uint64_t stride = (uint64_t)nq * gw;
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    uint32_t x = grp16;
+    for (; x + 3 * ngrp < gx; x += 4 * ngrp) {
+      a0 ^= p[x * stride];
+      a1 ^= p[(x + ngrp) * stride];
+      a2 ^= p[(x + 2 * ngrp) * stride];
+      a3 ^= p[(x + 3 * ngrp) * stride];
+    }
+    for (; x < gx; x += ngrp) a0 ^= p[x * stride];
+    acc = a0 ^ a1 ^ a2 ^ a3;
+  }
+  part[grp16][lane] = acc;
+  __syncthreads();
+  if (grp16 != 0 || idx >= (uint32_t)nq * words) return;
+  for (uint32_t gi = 1; gi < ngrp; ++gi) acc ^= part[gi][lane];
+  const uint32_t a = idx / words, w = idx - a * words;
   const uint32_t b0 = 4 * w;
   uint8_t* dst = out + (uint64_t)a * efs;
   if ((efs & 3u) == 0 && b0 + 4 <= efs) {
@@ -403,7 +427,6 @@ __global__ void k_reduce(const uint32_t* __restrict__ slabs, int nq, uint32_t gw
     for (uint32_t k = 0; k < 4; ++k)
       if (b0 + k < efs) dst[b0 + k] = (uint8_t)(acc >> (8 * k));
   }
-  (void)gy;
 }
 
 __global__ void k_xor_fold(const uint8_t* __restrict__ in, int nranks, size_t len,
@@ -479,22 +502,27 @@ hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys
   return hipGetLastError();
 }
 
-hipError_t launch_tree(const TreePlan& pl, const DevKey* d_key, uint4* d_front_s,
-                       uint32_t* d_front_t, uint8_t* d_c, int nrp, hipStream_t s,
-                       hipEvent_t mid) {
+hipError_t launch_frontier(const TreePlan& pl, const DevKey* d_key, uint4* d_front_s,
+                           uint32_t* d_front_t, hipStream_t s) {
   hipLaunchKernelGGL(k_tree_frontier, dim3(1u << pl.g), dim3(kTreeThreads), 0, s, d_key,
                      pl.prefix, pl.log_parts, pl.g, pl.e, d_front_s, d_front_t);
-  hipError_t err = hipGetLastError();
-  if (err != hipSuccess) return err;
-  if (mid) (void)hipEventRecord(mid, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_leaves(const TreePlan& pl, const DevKey* d_key, const uint4* d_front_s,
+                         const uint32_t* d_front_t, uint64_t f0, uint64_t nf, uint8_t* d_c,
+                         int nrp, hipStream_t s) {
   const int L0 = pl.log_parts + pl.g + pl.e;
-  const dim3 grid((unsigned)(pl.nfront / pl.tile));
+  const dim3 grid((unsigned)(nf / pl.tile));
+  const uint4* fs = d_front_s + f0;
+  const uint32_t* ft = d_front_t + f0;
+  uint8_t* c = d_c + (f0 << pl.d) * nrp;
   switch (nrp) {
-    case 1: hipLaunchKernelGGL(k_tree_leaves<1>, grid, dim3(kTreeThreads), 0, s, d_key, d_front_s, d_front_t, L0, pl.d, pl.tile, d_c); break;
-    case 2: hipLaunchKernelGGL(k_tree_leaves<2>, grid, dim3(kTreeThreads), 0, s, d_key, d_front_s, d_front_t, L0, pl.d, pl.tile, d_c); break;
-    case 4: hipLaunchKernelGGL(k_tree_leaves<4>, grid, dim3(kTreeThreads), 0, s, d_key, d_front_s, d_front_t, L0, pl.d, pl.tile, d_c); break;
-    case 8: hipLaunchKernelGGL(k_tree_leaves<8>, grid, dim3(kTreeThreads), 0, s, d_key, d_front_s, d_front_t, L0, pl.d, pl.tile, d_c); break;
-    case 16: hipLaunchKernelGGL(k_tree_leaves<16>, grid, dim3(kTreeThreads), 0, s, d_key, d_front_s, d_front_t, L0, pl.d, pl.tile, d_c); break;
+    case 1: hipLaunchKernelGGL(k_tree_leaves<1>, grid, dim3(kTreeThreads), 0, s, d_key, fs, ft, L0, pl.d, pl.tile, c); break;
+    case 2: hipLaunchKernelGGL(k_tree_leaves<2>, grid, dim3(kTreeThreads), 0, s, d_key, fs, ft, L0, pl.d, pl.tile, c); break;
+    case 4: hipLaunchKernelGGL(k_tree_leaves<4>, grid, dim3(kTreeThreads), 0, s, d_key, fs, ft, L0, pl.d, pl.tile, c); break;
+    case 8: hipLaunchKernelGGL(k_tree_leaves<8>, grid, dim3(kTreeThreads), 0, s, d_key, fs, ft, L0, pl.d, pl.tile, c); break;
+    case 16: hipLaunchKernelGGL(k_tree_leaves<16>, grid, dim3(kTreeThreads), 0, s, d_key, fs, ft, L0, pl.d, pl.tile, c); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -513,8 +541,8 @@ ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus) {
   const uint32_t gy = sh.uniform ? (sh.cpr + kColGroupLanes - 1) / kColGroupLanes : 1;
   const uint32_t rpw = sh.uniform ? 1 : kColGroupLanes / sh.cpr;
   const uint64_t groups = (nrec + rpw - 1) / rpw;
-  // enough waves to keep ~64 KiB of loads in flight per CU, at least a few groups per wave
-  const uint64_t want_blocks = (uint64_t)num_cus * 8;
+  // 16 waves per CU with 4 x 16 B loads in flight per lane (~64 KiB per CU), few slabs
+  const uint64_t want_blocks = (uint64_t)num_cus * kScanBlocksPerCU;
   const uint64_t waves_per_block = kScanThreads / 64;
   uint64_t gx = std::max<uint64_t>(1, std::min<uint64_t>(want_blocks / gy, (groups + 4 * waves_per_block - 1) / (4 * waves_per_block)));
   sh.grid = dim3((unsigned)gx, gy);
@@ -524,37 +552,38 @@ ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus) {
 
 template <int NQ>
 static hipError_t scan_nq(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
-                          const uint8_t* d_c, uint8_t* d_slabs, hipStream_t s) {
+                          const uint8_t* d_c, uint8_t* d_slabs, int acc, hipStream_t s) {
   constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : (NQ <= 8 ? 8 : 16)));
   constexpr int VEC = NQ <= 2 ? 4 : (NQ <= 8 ? 2 : 1);
   if (sh.uniform)
     hipLaunchKernelGGL((k_scan<NQ, NRP, VEC, true>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
-                       nrec, sh.pitch, sh.cpr, d_c, d_slabs);
+                       nrec, sh.pitch, sh.cpr, d_c, d_slabs, acc);
   else
     hipLaunchKernelGGL((k_scan<NQ, NRP, VEC, false>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
-                       nrec, sh.pitch, sh.cpr, d_c, d_slabs);
+                       nrec, sh.pitch, sh.cpr, d_c, d_slabs, acc);
   return hipGetLastError();
 }
 
 hipError_t launch_scan(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
-                       const uint8_t* d_c, uint8_t* d_slabs, hipStream_t s) {
+                       const uint8_t* d_c, uint8_t* d_slabs, bool accumulate, hipStream_t s) {
+  const int acc = accumulate ? 1 : 0;
   switch (sh.nq) {
-    case 1: return scan_nq<1>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 2: return scan_nq<2>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 3: return scan_nq<3>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 4: return scan_nq<4>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 5: return scan_nq<5>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 6: return scan_nq<6>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 7: return scan_nq<7>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 8: return scan_nq<8>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 9: return scan_nq<9>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 10: return scan_nq<10>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 11: return scan_nq<11>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 12: return scan_nq<12>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 13: return scan_nq<13>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 14: return scan_nq<14>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 15: return scan_nq<15>(sh, d_shard, nrec, d_c, d_slabs, s);
-    case 16: return scan_nq<16>(sh, d_shard, nrec, d_c, d_slabs, s);
+    case 1: return scan_nq<1>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 2: return scan_nq<2>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 3: return scan_nq<3>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 4: return scan_nq<4>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 5: return scan_nq<5>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 6: return scan_nq<6>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 7: return scan_nq<7>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 8: return scan_nq<8>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 9: return scan_nq<9>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 10: return scan_nq<10>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 11: return scan_nq<11>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 12: return scan_nq<12>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 13: return scan_nq<13>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 14: return scan_nq<14>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 15: return scan_nq<15>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+    case 16: return scan_nq<16>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -564,8 +593,8 @@ hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t e
   const uint32_t words = sh.pitch / 4;
   const uint32_t total = (uint32_t)sh.nq * words;
   const uint32_t gw = kColGroupLanes * sh.vec;
-  hipLaunchKernelGGL(k_reduce, dim3((total + 255) / 256), dim3(256), 0, s,
-                     reinterpret_cast<const uint32_t*>(d_slabs), sh.nq, gw, sh.grid.x, sh.grid.y,
+  hipLaunchKernelGGL(k_reduce, dim3((total + 63) / 64), dim3(kReduceThreads), 0, s,
+                     reinterpret_cast<const uint32_t*>(d_slabs), sh.nq, gw, sh.grid.x,
                      sh.pitch, efs, d_out);
   return hipGetLastError();
 }
