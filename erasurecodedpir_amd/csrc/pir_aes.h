@@ -1,12 +1,20 @@
-// pir_aes.h -- AES-128 for CDNA4: the PRG G of the reference (src/c/utils.cpp:37-51) is
+// pir_aes.h -- AES-128 for CDNA4.  The PRG G of the reference (src/c/utils.cpp:37-51) is
 // AES-128-CTR keyed by each tree node's seed, so there is no fixed key schedule to amortise:
-// every block runs the key schedule on the fly next to its rounds.
+// every node runs the key schedule on the fly next to its rounds.
 //
-// T-table form: one 1 KiB table Te0 (Te0[x] = {2S, S, S, 3S}, S = the FIPS-197 S-box, computed
-// on the host from the field definition) replicated 32x in LDS as [entry][lane & 31], so each
-// lane of a 32-lane ds_read_b32 group reads its own bank (conflict-free for any index pattern).
-// Te1..Te3 are byte rotations of Te0 (v_alignbit); the last round and the key schedule read
-// S = byte 1 of Te0.
+// T-box form with TWO LDS tables, Te0[x] = {2S,S,S,3S} and Te2 = rotl16(Te0) = {S,3S,2S,S}
+// (S = the FIPS-197 S-box, computed on the host from the field definition), each replicated
+// 32x as [entry][lane & 31]: every lane of a 32-lane ds_read_b32 group reads its own bank,
+// conflict-free for any index pattern.  With Te1 = rotl8(Te0) and Te3 = rotl8(Te2) a column is
+//     Te0[a] ^ Te2[c] ^ rotl8(Te0[b] ^ Te2[d] ^ rotr8(k))
+// -- one v_alignbit and two v_bitop3 (3-input XOR) per column.  The last round and the key
+// schedule read S from byte 1/2 of Te0 and byte 0/3 of Te2.
+//
+// Two execution shapes:
+//   * row shape (1 lane = 1 key): aes3_ctr() runs the 3 CTR blocks of an internal node
+//     (G(seed, blen<=48)) on one shared key schedule -- throughput levels;
+//   * column shape (4 lanes = 1 block, lane q holds column q; DPP quad permutes for ShiftRows
+//     and the key schedule's prefix XOR): aes_col() -- 4x lower latency for narrow levels.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -16,86 +24,150 @@ namespace pir {
 // Each translation unit that includes this header owns its own copy of the table.
 static __constant__ uint32_t c_te0[256];
 
-// ------------------------------------------------------------------------------------------
-// AES-128 encryption of one CTR block with an on-the-fly key schedule
-// ------------------------------------------------------------------------------------------
-struct Te {
-  const char* base;  // LDS table (byte address)
+constexpr uint32_t kTeBytes = 256 * 32 * 4;  // one replicated table: 32 KiB
+constexpr uint32_t kTablesBytes = 2 * kTeBytes;
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
+__device__ __forceinline__ uint32_t rotr8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 8); }
+
+// byte k of w -> byte offset of its table row (entry stride 128 B)
+__device__ __forceinline__ uint32_t off0(uint32_t w) { return (w << 7) & 0x7f80u; }
+__device__ __forceinline__ uint32_t off1(uint32_t w) { return (w >> 1) & 0x7f80u; }
+__device__ __forceinline__ uint32_t off2(uint32_t w) { return (w >> 9) & 0x7f80u; }
+__device__ __forceinline__ uint32_t off3(uint32_t w) { return (w >> 17) & 0x7f80u; }
+
+struct Tab {
+  const char* base;  // LDS: Te0 replicated, then Te2 replicated
   uint32_t lane4;    // (lane & 31) * 4
-  __device__ __forceinline__ uint32_t at(uint32_t off) const {
+  __device__ __forceinline__ uint32_t t0(uint32_t off) const {
     return *reinterpret_cast<const uint32_t*>(base + (off | lane4));
   }
-  // byte k of w -> offset of its Te0 row (entry stride 128 B)
-  __device__ __forceinline__ uint32_t b0(uint32_t w) const { return at((w << 7) & 0x7f80u); }
-  __device__ __forceinline__ uint32_t b1(uint32_t w) const { return at((w >> 1) & 0x7f80u); }
-  __device__ __forceinline__ uint32_t b2(uint32_t w) const { return at((w >> 9) & 0x7f80u); }
-  __device__ __forceinline__ uint32_t b3(uint32_t w) const { return at((w >> 17) & 0x7f80u); }
+  __device__ __forceinline__ uint32_t t2(uint32_t off) const {
+    return *reinterpret_cast<const uint32_t*>(base + kTeBytes + (off | lane4));
+  }
 };
 
-__device__ __forceinline__ uint32_t rotl(uint32_t x, int s) {
-  return __builtin_amdgcn_alignbit(x, x, 32 - s);
+// fill both replicated tables (all threads of the block)
+__device__ __forceinline__ void load_tables(uint32_t* lds) {
+  for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) {
+    const uint32_t v = c_te0[i >> 5];
+    lds[i] = v;
+    lds[256 * 32 + i] = __builtin_amdgcn_alignbit(v, v, 16);
+  }
 }
 
-// Te0[x] = {2S, S, S, 3S} (bytes 0..3); S[x] sits in byte 1.
-__device__ __forceinline__ uint32_t s_at0(uint32_t te) { return (te >> 8) & 0xffu; }
-__device__ __forceinline__ uint32_t s_at1(uint32_t te) { return te & 0xff00u; }
-__device__ __forceinline__ uint32_t s_at2(uint32_t te) { return (te << 8) & 0xff0000u; }
-__device__ __forceinline__ uint32_t s_at3(uint32_t te) { return (te << 16) & 0xff000000u; }
-
-__device__ __forceinline__ void key_step(const Te& T, uint32_t& k0, uint32_t& k1, uint32_t& k2,
+// SubWord(RotWord(k3)) ^ rcon, then the word chain (FIPS-197 5.2)
+__device__ __forceinline__ void key_next(const Tab& T, uint32_t& k0, uint32_t& k1, uint32_t& k2,
                                          uint32_t& k3, uint32_t rcon) {
-  // SubWord(RotWord(k3)) ^ rcon
-  uint32_t t = s_at0(T.b1(k3)) | s_at1(T.b2(k3)) | s_at2(T.b3(k3)) | s_at3(T.b0(k3));
-  k0 ^= t ^ rcon;
+  const uint32_t t = (T.t2(off1(k3)) & 0xffu) | (T.t0(off2(k3)) & 0xff00u) |
+                     (T.t0(off3(k3)) & 0xff0000u) | (T.t2(off0(k3)) & 0xff000000u);
+  k0 = xor3(k0, t, rcon);
   k1 ^= k0;
   k2 ^= k1;
   k3 ^= k2;
 }
 
-__device__ __forceinline__ void aes_round(const Te& T, uint32_t& w0, uint32_t& w1, uint32_t& w2,
-                                          uint32_t& w3, uint32_t k0, uint32_t k1, uint32_t k2,
-                                          uint32_t k3) {
-  uint32_t n0 = T.b0(w0) ^ rotl(T.b1(w1), 8) ^ rotl(T.b2(w2), 16) ^ rotl(T.b3(w3), 24) ^ k0;
-  uint32_t n1 = T.b0(w1) ^ rotl(T.b1(w2), 8) ^ rotl(T.b2(w3), 16) ^ rotl(T.b3(w0), 24) ^ k1;
-  uint32_t n2 = T.b0(w2) ^ rotl(T.b1(w3), 8) ^ rotl(T.b2(w0), 16) ^ rotl(T.b3(w1), 24) ^ k2;
-  uint32_t n3 = T.b0(w3) ^ rotl(T.b1(w0), 8) ^ rotl(T.b2(w1), 16) ^ rotl(T.b3(w2), 24) ^ k3;
+// one full round on a row-shape state; kr = rotr8 of the round key words
+__device__ __forceinline__ void round_row(const Tab& T, uint32_t& w0, uint32_t& w1, uint32_t& w2,
+                                          uint32_t& w3, uint32_t kr0, uint32_t kr1, uint32_t kr2,
+                                          uint32_t kr3) {
+  const uint32_t n0 = xor3(T.t0(off0(w0)), T.t2(off2(w2)), rotl8(xor3(T.t0(off1(w1)), T.t2(off3(w3)), kr0)));
+  const uint32_t n1 = xor3(T.t0(off0(w1)), T.t2(off2(w3)), rotl8(xor3(T.t0(off1(w2)), T.t2(off3(w0)), kr1)));
+  const uint32_t n2 = xor3(T.t0(off0(w2)), T.t2(off2(w0)), rotl8(xor3(T.t0(off1(w3)), T.t2(off3(w1)), kr2)));
+  const uint32_t n3 = xor3(T.t0(off0(w3)), T.t2(off2(w1)), rotl8(xor3(T.t0(off1(w0)), T.t2(off3(w2)), kr3)));
   w0 = n0; w1 = n1; w2 = n2; w3 = n3;
 }
 
-__device__ __forceinline__ void aes_last(const Te& T, uint32_t& w0, uint32_t& w1, uint32_t& w2,
-                                         uint32_t& w3, uint32_t k0, uint32_t k1, uint32_t k2,
-                                         uint32_t k3) {
-  uint32_t n0 = (s_at0(T.b0(w0)) | s_at1(T.b1(w1)) | s_at2(T.b2(w2)) | s_at3(T.b3(w3))) ^ k0;
-  uint32_t n1 = (s_at0(T.b0(w1)) | s_at1(T.b1(w2)) | s_at2(T.b2(w3)) | s_at3(T.b3(w0))) ^ k1;
-  uint32_t n2 = (s_at0(T.b0(w2)) | s_at1(T.b1(w3)) | s_at2(T.b2(w0)) | s_at3(T.b3(w1))) ^ k2;
-  uint32_t n3 = (s_at0(T.b0(w3)) | s_at1(T.b1(w0)) | s_at2(T.b2(w1)) | s_at3(T.b3(w2))) ^ k3;
-  w0 = n0; w1 = n1; w2 = n2; w3 = n3;
+// last-round column from (w_c, w_c+1, w_c+2, w_c+3): SubBytes + ShiftRows + AddRoundKey
+__device__ __forceinline__ uint32_t last_col(const Tab& T, uint32_t a, uint32_t b, uint32_t c,
+                                             uint32_t d, uint32_t k) {
+  uint32_t x = (T.t2(off0(a)) & 0xffu) | (T.t0(off1(b)) & 0xff00u);
+  x |= (T.t0(off2(c)) & 0xff0000u) | (T.t2(off3(d)) & 0xff000000u);
+  return x ^ k;
 }
 
-// AES-128_key(BE128(ctr)), ctr < 256: the ctr-th 16-byte block of G(key, .) (utils.cpp:37-51)
-__device__ __forceinline__ uint4 aes_ctr_block(const Te& T, uint4 key, uint32_t ctr) {
+constexpr uint32_t kRcon[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
+
+// Row shape, one key, NB CTR blocks with counters 0..NB-1; block NB-1 only needs its first
+// LASTW output words (the control-bit bytes); out[b] = AES_key(BE128(b)).
+template <int NB, int LASTW>
+__device__ __forceinline__ void aes_ctr_row(const Tab& T, uint4 key, uint4 (&out)[NB]) {
   uint32_t k0 = key.x, k1 = key.y, k2 = key.z, k3 = key.w;
-  uint32_t w0 = k0, w1 = k1, w2 = k2, w3 = k3 ^ (ctr << 24);
-  constexpr uint32_t rc[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
+  uint32_t w[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    w[b][0] = k0; w[b][1] = k1; w[b][2] = k2; w[b][3] = k3 ^ ((uint32_t)b << 24);
+  }
 #pragma unroll
   for (int r = 0; r < 9; ++r) {
-    key_step(T, k0, k1, k2, k3, rc[r]);
-    aes_round(T, w0, w1, w2, w3, k0, k1, k2, k3);
+    key_next(T, k0, k1, k2, k3, kRcon[r]);
+    const uint32_t r0 = rotr8(k0), r1 = rotr8(k1), r2 = rotr8(k2), r3 = rotr8(k3);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) round_row(T, w[b][0], w[b][1], w[b][2], w[b][3], r0, r1, r2, r3);
   }
-  key_step(T, k0, k1, k2, k3, rc[9]);
-  aes_last(T, w0, w1, w2, w3, k0, k1, k2, k3);
-  return make_uint4(w0, w1, w2, w3);
+  key_next(T, k0, k1, k2, k3, kRcon[9]);
+  const uint32_t kk[4] = {k0, k1, k2, k3};
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    uint32_t o[4] = {0, 0, 0, 0};
+    const int nw = (b == NB - 1) ? LASTW : 4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < nw) o[c] = last_col(T, w[b][c], w[b][(c + 1) & 3], w[b][(c + 2) & 3], w[b][(c + 3) & 3], kk[c]);
+    out[b] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
 }
 
-__device__ __forceinline__ void load_te_lds(uint32_t* lds_te) {
-  for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) lds_te[i] = c_te0[i >> 5];
+// Row shape, one block with counter `ctr` (generic helper, e.g. key generation).
+__device__ __forceinline__ uint4 aes_ctr_block(const Tab& T, uint4 key, uint32_t ctr) {
+  uint32_t k0 = key.x, k1 = key.y, k2 = key.z, k3 = key.w;
+  uint32_t w0 = k0, w1 = k1, w2 = k2, w3 = k3 ^ (ctr << 24);
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    key_next(T, k0, k1, k2, k3, kRcon[r]);
+    round_row(T, w0, w1, w2, w3, rotr8(k0), rotr8(k1), rotr8(k2), rotr8(k3));
+  }
+  key_next(T, k0, k1, k2, k3, kRcon[9]);
+  return make_uint4(last_col(T, w0, w1, w2, w3, k0), last_col(T, w1, w2, w3, w0, k1),
+                    last_col(T, w2, w3, w0, w1, k2), last_col(T, w3, w0, w1, w2, k3));
 }
 
-__device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
-  return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+// ---- column shape: 4 lanes (a DPP quad) per block, lane q = column q ----------------------
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
 }
-__device__ __forceinline__ uint4 and4(uint4 a, uint32_t m) {
-  return make_uint4(a.x & m, a.y & m, a.z & m, a.w & m);
+constexpr int kQ1230 = 0x39;  // lane q reads q+1
+constexpr int kQ2301 = 0x4E;  // q+2
+constexpr int kQ3012 = 0x93;  // q+3
+constexpr int kQ3333 = 0xFF;  // lane 3
+constexpr int kQ0012 = 0x90;  // q-1 (lane 0 reads itself)
+constexpr int kQ0101 = 0x44;  // q-2 (lanes 0,1 read themselves)
+
+// AES-128_k(pt) where lane q holds key word k_q and plaintext word pt_q; returns ciphertext
+// word q.  All 4 lanes of the quad must be active.  mq1/mq2: all-ones when q >= 1 / q >= 2.
+__device__ __forceinline__ uint32_t aes_col(const Tab& T, uint32_t kq, uint32_t ptq, uint32_t mq1,
+                                            uint32_t mq2) {
+  uint32_t w = kq ^ ptq;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    // key schedule: k'_q = SubWordRot(k3) ^ rcon ^ (k_0 ^ ... ^ k_q)
+    const uint32_t k3 = qperm<kQ3333>(kq);
+    const uint32_t t = (T.t2(off1(k3)) & 0xffu) | (T.t0(off2(k3)) & 0xff00u) |
+                       (T.t0(off3(k3)) & 0xff0000u) | (T.t2(off0(k3)) & 0xff000000u);
+    uint32_t pre = kq ^ (qperm<kQ0012>(kq) & mq1);
+    pre ^= qperm<kQ0101>(pre) & mq2;
+    kq = xor3(pre, t, kRcon[r]);
+    const uint32_t b = qperm<kQ1230>(w), c = qperm<kQ2301>(w), d = qperm<kQ3012>(w);
+    if (r < 9)
+      w = xor3(T.t0(off0(w)), T.t2(off2(c)), rotl8(xor3(T.t0(off1(b)), T.t2(off3(d)), rotr8(kq))));
+    else
+      w = last_col(T, w, b, c, d, kq);
+  }
+  return w;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -132,6 +204,13 @@ static inline void upload_te0(hipStream_t s) {
   }
   (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_te0), te0, sizeof(te0), 0, hipMemcpyHostToDevice, s);
   (void)hipStreamSynchronize(s);
+}
+
+__device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
+  return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+}
+__device__ __forceinline__ uint4 and4(uint4 a, uint32_t m) {
+  return make_uint4(a.x & m, a.y & m, a.z & m, a.w & m);
 }
 
 }  // namespace pir

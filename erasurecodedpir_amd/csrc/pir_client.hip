@@ -16,7 +16,7 @@ namespace pir {
 namespace {
 
 struct KeygenSmem {
-  uint32_t te[256 * 32];
+  uint32_t tab[2 * 256 * 32];
   uint4 s[PIR_MAX_PARTIES];
   uint32_t t[PIR_MAX_PARTIES];
   uint4 out[PIR_MAX_PARTIES][3];
@@ -40,8 +40,8 @@ __global__ __launch_bounds__(64) void k_keygen(int n, uint64_t index, const uint
                                                int p, int nq, const uint8_t* __restrict__ seeds,
                                                uint8_t* __restrict__ keys, int kl) {
   __shared__ KeygenSmem sm;
-  load_te_lds(sm.te);
-  const Te T{reinterpret_cast<const char*>(sm.te), (threadIdx.x & 31u) * 4u};
+  load_tables(sm.tab);
+  const Tab T{reinterpret_cast<const char*>(sm.tab), (threadIdx.x & 31u) * 4u};
   const int tid = threadIdx.x, pm1 = p - 1, CWk = 16 + 2 * p - 2, CW = pm1 * CWk;
   const uint32_t tbits = 2 * pm1;
   const uint32_t tb_mask = tbits >= 32 ? 0xffffffffu : ((1u << tbits) - 1u);

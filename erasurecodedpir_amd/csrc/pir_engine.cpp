@@ -88,8 +88,7 @@ struct pir_engine {
   uint8_t* d_key_raw = nullptr;  // max_batch keys
   pir::DevKey* d_keys = nullptr; // max_batch parsed keys
   int max_batch = 0;
-  uint4* d_front_s = nullptr;
-  uint32_t* d_front_t = nullptr;
+  pir::NodeBufs nodes{};  // tree levels between kernels (ping-pong)
   uint8_t* d_c = nullptr;
   uint8_t* d_slabs = nullptr;
   size_t slab_cap = 0;
@@ -138,9 +137,9 @@ int ensure_slabs(pir_engine* e, size_t bytes) {
 
 int pick_chunks(const pir::TreePlan& pl) {
   // pipeline only when every chunk still fills the GPU (>= 2^16 records)
+  const int cmax = std::min(kMaxChunks, pir::max_chunks(pl));
   int c = 1;
-  while (c < kMaxChunks && (pl.nfront / pl.tile) % (2 * c) == 0 && (pl.nleaves >> 16) >= (uint64_t)(2 * c))
-    c *= 2;
+  while (2 * c <= cmax && (pl.nleaves >> 16) >= (uint64_t)(2 * c)) c *= 2;
   return c;
 }
 
@@ -154,18 +153,17 @@ int answer_core(pir_engine* e, const pir::DevKey* d_key, int log_parts_total, ui
   const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix);
   const int C = pick_chunks(pl);
   e->last_chunks = C;
-  const uint64_t nrec = pl.nleaves / C, nfc = pl.nfront / C;
+  const uint64_t nrec = pl.nleaves / C;
   const pir::ScanShape sh = pir::make_scan_shape(nrec, e->pitch, c.num_rounds, e->num_cus);
   int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
   if (rc) return rc;
   hipEvent_t* ev = e->ev;
   if (ev) HIP_TRY(hipEventRecord(ev[EV_KEY], s));
-  HIP_TRY(pir::launch_frontier(pl, d_key, e->d_front_s, e->d_front_t, s));
+  HIP_TRY(pir::launch_frontier(pl, d_key, e->nodes, s));
   if (ev) HIP_TRY(hipEventRecord(ev[EV_FRONT], s));
   for (int j = 0; j < C; ++j) {
     if (ev) HIP_TRY(hipEventRecord(ev[EV_LEAF_B + j], s));
-    HIP_TRY(pir::launch_leaves(pl, d_key, e->d_front_s, e->d_front_t, j * nfc, nfc, e->d_c,
-                               e->nrp, s));
+    HIP_TRY(pir::launch_stages(pl, d_key, e->nodes, j, C, e->d_c, e->nrp, s));
     if (ev) HIP_TRY(hipEventRecord(ev[EV_LEAF_E + j], s));
     HIP_TRY(hipEventRecord(e->ev_leaf[j], s));
     HIP_TRY(hipStreamWaitEvent(e->aux, e->ev_leaf[j], 0));
@@ -313,8 +311,10 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
     return cleanup(fail(PIR_EHIP, "hipMemset shard"));
   const pir::TreePlan pl = pir::make_plan(c.log_num_records, c.log_num_partitions, 0);
   const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
-  if (hipMalloc(&e->d_front_s, pl.nfront * sizeof(uint4)) != hipSuccess ||
-      hipMalloc(&e->d_front_t, pl.nfront * sizeof(uint32_t)) != hipSuccess ||
+  if (hipMalloc(&e->nodes.s[0], pl.max_nodes * sizeof(uint4)) != hipSuccess ||
+      hipMalloc(&e->nodes.s[1], pl.max_nodes * sizeof(uint4)) != hipSuccess ||
+      hipMalloc(&e->nodes.t[0], pl.max_nodes * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&e->nodes.t[1], pl.max_nodes * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&e->d_c, (size_t)e->rows * e->nrp) != hipSuccess ||
       hipMalloc(&e->d_part, out_bytes) != hipSuccess ||
       hipMalloc(&e->d_result, out_bytes) != hipSuccess ||
@@ -334,8 +334,9 @@ void pir_engine_destroy(pir_engine_t* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->aux) (void)hipStreamSynchronize(e->aux);
   if (e->comm) (void)ncclCommDestroy(e->comm);
-  for (auto* p : {(void*)e->d_shard, (void*)e->d_key_raw, (void*)e->d_keys, (void*)e->d_front_s,
-                  (void*)e->d_front_t, (void*)e->d_c, (void*)e->d_slabs, (void*)e->d_part,
+  for (auto* p : {(void*)e->d_shard, (void*)e->d_key_raw, (void*)e->d_keys,
+                  (void*)e->nodes.s[0], (void*)e->nodes.s[1], (void*)e->nodes.t[0],
+                  (void*)e->nodes.t[1], (void*)e->d_c, (void*)e->d_slabs, (void*)e->d_part,
                   (void*)e->d_gather, (void*)e->d_result})
     if (p) (void)hipFree(p);
   for (auto& b : e->user) (void)hipFree(b.p);
@@ -493,7 +494,8 @@ int pir_engine_eval_all(pir_engine_t* e, const uint8_t* key, uint8_t* out) {
                                c.num_rounds, c.party_index - 1, e->d_keys, e->stream));
   const pir::TreePlan pl =
       pir::make_plan(c.log_num_records, c.log_num_partitions, (uint64_t)c.partition_index);
-  HIP_TRY(pir::launch_tree(pl, e->d_keys, e->d_front_s, e->d_front_t, e->d_c, e->nrp, e->stream));
+  HIP_TRY(pir::launch_frontier(pl, e->d_keys, e->nodes, e->stream));
+  HIP_TRY(pir::launch_stages(pl, e->d_keys, e->nodes, 0, 1, e->d_c, e->nrp, e->stream));
   std::vector<uint8_t> ct((size_t)e->rows * e->nrp);
   HIP_TRY(hipMemcpyAsync(ct.data(), e->d_c, ct.size(), hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));

@@ -8,8 +8,6 @@ namespace pir {
 
 constexpr int kMaxLevels = 40;  // PIR_MAX_LOG_RECORDS
 constexpr int kMaxCW = 16;      // p - 1 <= 16
-constexpr int kNodeCap = 1024;  // tree nodes per LDS level buffer
-constexpr int kTreeThreads = 512;
 constexpr int kScanThreads = 512;
 constexpr int kScanBlocksPerCU = 2;
 constexpr int kReduceThreads = 1024;
@@ -26,37 +24,41 @@ struct DevKey {
   uint4 lastcw[kMaxCW];                // lastCW[j][a] as byte a (a < nq; zero above)
 };
 
-// Key-independent shape of one answer pass (one partition of the logical tree).
+// Key-independent shape of one answer pass (one partition of the logical tree):
+//   k_frontier  : levels [0, log_parts + F) -> 2^F nodes (latency-bound, column-shape AES)
+//   stages      : k_expand, <= 4 levels each; the last one converts the leaves
+struct Stage {
+  int L_in;      // absolute tree level of the stage's input nodes
+  int k;         // levels expanded
+  int tile;      // input nodes per workgroup
+  uint64_t nin;  // input nodes (whole partition)
+  bool final;
+};
 struct TreePlan {
-  int n;            // full tree depth (LOG_NUM_ENCODED_FILES)
-  int log_parts;    // partition prefix depth
-  uint64_t prefix;  // partition index (path bits MSB first)
-  int g;            // frontier kernel: 2^g workgroups, each descends g more levels
-  int e;            // ... then expands e levels (frontier level F = log_parts + g + e)
-  int d;            // leaves kernel: expands d levels below the frontier
-  int tile;         // frontier nodes per leaves-kernel workgroup
-  uint64_t nfront;  // 2^(g+e)
-  uint64_t nleaves; // 2^(n - log_parts)
+  int n, log_parts;
+  uint64_t prefix;
+  int F, g, e;  // frontier: 2^g workgroups, each descends log_parts+g levels, expands e
+  uint64_t nfront, nleaves, max_nodes;
+  int nstages;
+  Stage st[8];
+};
+struct NodeBufs {  // ping-pong node arrays in global memory (max_nodes entries each)
+  uint4* s[2];
+  uint32_t* t[2];
 };
 
 TreePlan make_plan(int n, int log_parts, uint64_t prefix);
+int max_chunks(const TreePlan& pl);
 
 void upload_aes_table(hipStream_t s);  // Te0 (computed on the host) -> __constant__ memory
 
 hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys, int p, int n,
                            int nq, int party0, DevKey* d_keys, hipStream_t s);
-hipError_t launch_frontier(const TreePlan& pl, const DevKey* d_key, uint4* d_front_s,
-                           uint32_t* d_front_t, hipStream_t s);
-// leaves of frontier nodes [f0, f0 + nf) (nf a multiple of pl.tile) -> c rows [f0<<d, ...)
-hipError_t launch_leaves(const TreePlan& pl, const DevKey* d_key, const uint4* d_front_s,
-                         const uint32_t* d_front_t, uint64_t f0, uint64_t nf, uint8_t* d_c,
-                         int nrp, hipStream_t s);
-inline hipError_t launch_tree(const TreePlan& pl, const DevKey* d_key, uint4* d_front_s,
-                              uint32_t* d_front_t, uint8_t* d_c, int nrp, hipStream_t s) {
-  hipError_t e = launch_frontier(pl, d_key, d_front_s, d_front_t, s);
-  if (e != hipSuccess) return e;
-  return launch_leaves(pl, d_key, d_front_s, d_front_t, 0, pl.nfront, d_c, nrp, s);
-}
+hipError_t launch_frontier(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb,
+                           hipStream_t s);
+// the expand stages of chunk j of C -> c rows of that chunk's leaves
+hipError_t launch_stages(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb, int j, int C,
+                         uint8_t* d_c, int nrp, hipStream_t s);
 // scan rows [0, nrec) of `shard` (row pitch `pitch`) with coefficients cT[i*nrp + a]
 struct ScanShape {
   int nq, nrp, vec;      // vec = dwords per lane chunk (4, 2, 1)

@@ -21,49 +21,6 @@ namespace pir {
 
 void upload_aes_table(hipStream_t s) { upload_te0(s); }
 
-// One third of a node expansion (dpf_tree.cpp:530-551).  role 0 / 1: the corrected left /
-// right child seed; role 2: packed child control bits (bits [0,p-1) left, [p-1,2p-2) right).
-__device__ __forceinline__ uint4 expand_role(const Te& T, const DevKey* __restrict__ K, int L,
-                                            uint4 seed, uint32_t t, int role, uint32_t pm1,
-                                            uint32_t tb_mask) {
-  uint4 o = aes_ctr_block(T, seed, (uint32_t)role);
-  uint4 cs = make_uint4(0, 0, 0, 0);
-  uint32_t ct = 0;
-  for (uint32_t j = 0; j < pm1; ++j) {  // parse_prg_output t bits + CW (dpf_tree.cpp:533-541)
-    uint32_t m = 0u - ((t >> j) & 1u);
-    cs = xor4(cs, and4(K->scw[L * kMaxCW + j], m));
-    ct ^= K->tcw[L * kMaxCW + j] & m;
-  }
-  if (role < 2) return xor4(o, cs);
-  o.x = (o.x & tb_mask) ^ ct;
-  return o;
-}
-
-struct TreeSmem {
-  uint32_t te[256 * 32];
-  uint4 s[2][kNodeCap];
-  uint32_t t[2][kNodeCap];
-};
-
-// One level of expansions inside a workgroup: parents in[off, off+W) -> children.
-// Children go to LDS buffer `out` (to_global == false) or to the global frontier arrays.
-__device__ __forceinline__ void expand_level(const Te& T, const DevKey* __restrict__ K, int L,
-                                             const uint4* in_s, const uint32_t* in_t, int off,
-                                             int W, uint4* out_s, uint32_t* out_t, uint32_t pm1,
-                                             uint32_t tb_mask) {
-  const uint32_t tmask = (1u << pm1) - 1u;
-  for (int task = threadIdx.x; task < 3 * W; task += blockDim.x) {
-    const int u = task / 3, r = task - 3 * u;
-    uint4 o = expand_role(T, K, L, in_s[off + u], in_t[off + u], r, pm1, tb_mask);
-    if (r < 2) {
-      out_s[2 * u + r] = o;
-    } else {
-      out_t[2 * u] = o.x & tmask;
-      out_t[2 * u + 1] = (o.x >> pm1) & tmask;
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------
 // k_key_prep: raw key bytes -> DevKey (one workgroup per key)
 // ------------------------------------------------------------------------------------------
@@ -103,125 +60,260 @@ __global__ __launch_bounds__(256) void k_key_prep(const uint8_t* __restrict__ ra
 }
 
 // ------------------------------------------------------------------------------------------
-// k_tree_frontier: each of 2^g workgroups descends from the root along
-// (prefix << g | blockIdx.x) for log_parts + g levels (3 lanes per node: one AES block
-// each), then expands e levels breadth-first in LDS; the last level goes to global memory.
+// Correction words of one level for a node with control bits t (dpf_tree.cpp:533-541):
+//   cs = XOR_{j: t_j} sCW[L][j]   (applied to both child seeds)
+//   ct = XOR_{j: t_j} tCW[L][j]   (applied to the packed child control bits)
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kTreeThreads) void k_tree_frontier(
-    const DevKey* __restrict__ K, uint64_t prefix, int log_parts, int g, int e,
-    uint4* __restrict__ front_s, uint32_t* __restrict__ front_t) {
-  __shared__ TreeSmem sm;
-  load_te_lds(sm.te);
-  const Te T{reinterpret_cast<const char*>(sm.te), (threadIdx.x & 31u) * 4u};
-  const uint32_t pm1 = K->p - 1;
-  const uint32_t tbits = 2 * pm1;
-  const uint32_t tb_mask = tbits >= 32 ? 0xffffffffu : ((1u << tbits) - 1u);
-  if (threadIdx.x == 0) {
-    sm.s[0][0] = K->root_seed;
-    sm.t[0][0] = K->root_t;
+__device__ __forceinline__ void level_cw(const DevKey* __restrict__ K, int L, uint32_t t,
+                                         uint32_t pm1, uint4& cs, uint32_t& ct) {
+  cs = make_uint4(0, 0, 0, 0);
+  ct = 0;
+  for (uint32_t j = 0; j < pm1; ++j) {
+    const uint32_t m = 0u - ((t >> j) & 1u);
+    cs = xor4(cs, and4(K->scw[L * kMaxCW + j], m));
+    ct ^= K->tcw[L * kMaxCW + j] & m;
   }
+}
+
+struct Bits {
+  uint32_t pm1, tmask, tb_mask;
+  __device__ explicit Bits(uint32_t p) {
+    pm1 = p - 1;
+    tmask = (1u << pm1) - 1u;
+    tb_mask = 2 * pm1 >= 32 ? 0xffffffffu : ((1u << (2 * pm1)) - 1u);
+  }
+};
+
+// ------------------------------------------------------------------------------------------
+// k_frontier: the narrow, latency-bound top of the tree.  Each of 2^g workgroups descends from
+// the root along (prefix << g | blockIdx.x) for log_parts + g levels, then expands e levels
+// breadth-first; the 2^e nodes of the last level go to global memory.  Column-shape AES: a
+// node is 16 lanes = 4 quads, quad r computes CTR block r of G(seed) (quad 3 is a spare), so
+// one expansion costs ~1/4 of a row-shape block's latency.  During the descent every 16-lane
+// group computes the same node (no barrier: the chosen child is fetched with __shfl).
+// ------------------------------------------------------------------------------------------
+constexpr int kFrontThreads = 512;
+constexpr int kFrontCap = 256;  // nodes per LDS level buffer (e <= 9)
+struct FrontSmem {
+  uint32_t tab[2 * 256 * 32];
+  uint32_t s[2][kFrontCap][4];
+  uint32_t t[2][kFrontCap];
+};
+
+__device__ __forceinline__ uint32_t word_of(const uint4& v, uint32_t q) {
+  return q == 0 ? v.x : (q == 1 ? v.y : (q == 2 ? v.z : v.w));
+}
+
+__global__ __launch_bounds__(kFrontThreads) void k_frontier(
+    const DevKey* __restrict__ K, uint64_t prefix, int log_parts, int g, int e,
+    uint4* __restrict__ out_s, uint32_t* __restrict__ out_t) {
+  __shared__ FrontSmem sm;
+  load_tables(sm.tab);
+  const Tab T{reinterpret_cast<const char*>(sm.tab), (threadIdx.x & 31u) * 4u};
+  const Bits B(K->p);
+  const uint32_t q = threadIdx.x & 3u, role = (threadIdx.x >> 2) & 3u;
+  const uint32_t mq1 = q >= 1 ? 0xffffffffu : 0u, mq2 = q >= 2 ? 0xffffffffu : 0u;
+  const uint32_t ptq = q == 3 ? (role << 24) : 0u;  // CTR block `role`: BE128(role)
+  const int lane = threadIdx.x & 63;
+  const int g16 = lane & ~15;
   __syncthreads();
+
+  // ---- descent (redundant in every 16-lane group) --------------------------------------
   const int D0 = log_parts + g;
   const uint64_t path = (prefix << g) | blockIdx.x;
-  int cur = 0, pidx = 0;
-  for (int L = 0; L < D0; ++L) {  // descent (cf. the intended dpf_tree.cpp:657-684)
-    if (threadIdx.x < 3) {
-      const int r = threadIdx.x;
-      uint4 o = expand_role(T, K, L, sm.s[cur][pidx], sm.t[cur][pidx], r, pm1, tb_mask);
-      if (r < 2) {
-        sm.s[cur ^ 1][r] = o;
-      } else {
-        const uint32_t tmask = (1u << pm1) - 1u;
-        sm.t[cur ^ 1][0] = o.x & tmask;
-        sm.t[cur ^ 1][1] = (o.x >> pm1) & tmask;
+  uint32_t sq = word_of(K->root_seed, q), t = K->root_t;
+  for (int L = 0; L < D0; ++L) {
+    const uint32_t o = aes_col(T, sq, ptq, mq1, mq2);
+    uint4 cs;
+    uint32_t ct;
+    level_cw(K, L, t, B.pm1, cs, ct);
+    const uint32_t bit = (uint32_t)((path >> (D0 - 1 - L)) & 1u);
+    const uint32_t oc = o ^ word_of(cs, q);
+    sq = (uint32_t)__shfl((int)oc, g16 | (int)(bit << 2) | (int)q, 64);
+    const uint32_t tb = ((uint32_t)__shfl((int)o, g16 | 8, 64) & B.tb_mask) ^ ct;
+    t = (tb >> (bit * B.pm1)) & B.tmask;
+  }
+  const uint64_t obase = (uint64_t)blockIdx.x << e;
+  if (e == 0) {
+    if (threadIdx.x < 4) reinterpret_cast<uint32_t*>(out_s + blockIdx.x)[q] = sq;
+    if (threadIdx.x == 0) out_t[blockIdx.x] = t;
+    return;
+  }
+  if (threadIdx.x < 4) sm.s[0][0][q] = sq;
+  if (threadIdx.x == 0) sm.t[0][0] = t;
+  __syncthreads();
+
+  // ---- breadth-first expansion, 32 nodes per pass ----------------------------------------
+  int cur = 0, W = 1;
+  for (int lv = 0; lv < e; ++lv) {
+    const int L = D0 + lv;
+    const bool last = lv == e - 1;
+    for (int u0 = 0; u0 < W; u0 += kFrontThreads / 16) {
+      const int u = u0 + (int)(threadIdx.x >> 4);
+      if (u < W) {  // uniform per 16-lane group (DPP stays inside a quad)
+        const uint32_t s_in = sm.s[cur][u][q], t_in = sm.t[cur][u];
+        const uint32_t o = aes_col(T, s_in, ptq, mq1, mq2);
+        uint4 cs;
+        uint32_t ct;
+        level_cw(K, L, t_in, B.pm1, cs, ct);
+        if (role < 2) {
+          const uint32_t v = o ^ word_of(cs, q);
+          if (last) reinterpret_cast<uint32_t*>(out_s + obase + 2 * u + role)[q] = v;
+          else sm.s[cur ^ 1][2 * u + role][q] = v;
+        } else if (role == 2 && q == 0) {
+          const uint32_t tb = (o & B.tb_mask) ^ ct;
+          const uint32_t tl = tb & B.tmask, tr = (tb >> B.pm1) & B.tmask;
+          if (last) {
+            out_t[obase + 2 * u] = tl;
+            out_t[obase + 2 * u + 1] = tr;
+          } else {
+            sm.t[cur ^ 1][2 * u] = tl;
+            sm.t[cur ^ 1][2 * u + 1] = tr;
+          }
+        }
       }
     }
     __syncthreads();
     cur ^= 1;
-    pidx = (int)((path >> (D0 - 1 - L)) & 1u);
-  }
-  const uint64_t base = (uint64_t)blockIdx.x << e;
-  if (e == 0) {
-    if (threadIdx.x == 0) {
-      front_s[blockIdx.x] = sm.s[cur][pidx];
-      front_t[blockIdx.x] = sm.t[cur][pidx];
-    }
-    return;
-  }
-  int W = 1, off = pidx;
-  for (int lv = 0; lv < e; ++lv) {
-    const int L = D0 + lv;
-    if (lv == e - 1) {
-      expand_level(T, K, L, sm.s[cur], sm.t[cur], off, W, front_s + base, front_t + base, pm1,
-                   tb_mask);
-    } else {
-      expand_level(T, K, L, sm.s[cur], sm.t[cur], off, W, sm.s[cur ^ 1], sm.t[cur ^ 1], pm1,
-                   tb_mask);
-      __syncthreads();
-      cur ^= 1;
-      W *= 2;
-      off = 0;
-    }
+    W *= 2;
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// k_tree_leaves: `tile` frontier nodes per workgroup, d more levels in LDS, then every leaf
-// j gives c[j][a] = AES_{s_j}(0)[a] ^ XOR_{k: t_j bit k} lastCW[k][a]  (dpf_tree.cpp:567-580)
-// c layout: row-major [leaf][nrp] bytes (nrp = pow2 >= nq, unused bytes zero).
+// k_expand: the wide, throughput-bound levels.  A workgroup takes `tile` nodes of level L0 and
+// expands k levels breadth-first in LDS, one lane per node (row-shape AES: the 3 CTR blocks of
+// G(seed) share one key schedule).  FINAL: the last level is fused with the leaf conversion
+// (dpf_tree.cpp:567-580): each lane expands a parent and converts both children,
+//   c[leaf][a] = AES_{s_leaf}(0)[a] ^ XOR_{k: t_leaf bit k} lastCW[k][a]   (a < nq),
+// written as rows of NRP bytes (nq padded to a power of two, pad bytes zero).
+// !FINAL: the last level's nodes go to global memory for the next stage.
 // ------------------------------------------------------------------------------------------
+constexpr int kExpThreads = 1024;
+constexpr int kExpOut = 4096;  // nodes produced per workgroup (tile << k)
+struct ExpSmem {
+  uint32_t tab[2 * 256 * 32];
+  uint4 sa[kExpOut / 2];
+  uint32_t ta[kExpOut / 2];
+  uint4 sb[kExpOut / 4];
+  uint32_t tb[kExpOut / 4];
+};
+
+// G(seed) of an internal node with corrections: children seeds and control bits
+__device__ __forceinline__ void expand_node(const Tab& T, const DevKey* __restrict__ K, int L,
+                                            const Bits& B, uint4 seed, uint32_t t, uint4& sl,
+                                            uint4& sr, uint32_t& tl, uint32_t& tr) {
+  uint4 o[3];
+  aes_ctr_row<3, 1>(T, seed, o);
+  uint4 cs;
+  uint32_t ct;
+  level_cw(K, L, t, B.pm1, cs, ct);
+  sl = xor4(o[0], cs);
+  sr = xor4(o[1], cs);
+  const uint32_t tb = (o[2].x & B.tb_mask) ^ ct;
+  tl = tb & B.tmask;
+  tr = (tb >> B.pm1) & B.tmask;
+}
+
 template <int NRP>
-__global__ __launch_bounds__(kTreeThreads) void k_tree_leaves(
-    const DevKey* __restrict__ K, const uint4* __restrict__ front_s,
-    const uint32_t* __restrict__ front_t, int L0, int d, int tile, uint8_t* __restrict__ c) {
-  __shared__ TreeSmem sm;
-  load_te_lds(sm.te);
-  const Te T{reinterpret_cast<const char*>(sm.te), (threadIdx.x & 31u) * 4u};
-  const uint32_t pm1 = K->p - 1;
-  const uint32_t tbits = 2 * pm1;
-  const uint32_t tb_mask = tbits >= 32 ? 0xffffffffu : ((1u << tbits) - 1u);
-  const uint64_t fbase = (uint64_t)blockIdx.x * tile;
-  for (int i = threadIdx.x; i < tile; i += blockDim.x) {
-    sm.s[0][i] = front_s[fbase + i];
-    sm.t[0][i] = front_t[fbase + i];
-  }
-  __syncthreads();
-  int cur = 0, W = tile;
-  for (int lv = 0; lv < d; ++lv) {
-    expand_level(T, K, L0 + lv, sm.s[cur], sm.t[cur], 0, W, sm.s[cur ^ 1], sm.t[cur ^ 1], pm1,
-                 tb_mask);
-    __syncthreads();
-    cur ^= 1;
-    W *= 2;
-  }
-  const uint32_t nq = K->nq;
-  uint4 qmask;  // keep bytes a < nq
+__device__ __forceinline__ void store_leaf(uint8_t* __restrict__ c, uint64_t leaf, uint4 v) {
+  uint8_t* dst = c + leaf * NRP;
+  if constexpr (NRP == 1) *dst = (uint8_t)v.x;
+  else if constexpr (NRP == 2) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)v.x;
+  else if constexpr (NRP == 4) *reinterpret_cast<uint32_t*>(dst) = v.x;
+  else if constexpr (NRP == 8) *reinterpret_cast<uint2*>(dst) = make_uint2(v.x, v.y);
+  else *reinterpret_cast<uint4*>(dst) = v;
+}
+
+// leaf value (before masking to nq bytes)
+template <int NW>
+__device__ __forceinline__ uint4 leaf_value(const Tab& T, const DevKey* __restrict__ K,
+                                            uint32_t pm1, uint4 seed, uint32_t t) {
+  uint4 o[1];
+  aes_ctr_row<1, NW>(T, seed, o);
+  for (uint32_t j = 0; j < pm1; ++j) o[0] = xor4(o[0], and4(K->lastcw[j], 0u - ((t >> j) & 1u)));
+  return o[0];
+}
+
+template <bool FINAL, int NRP>
+__global__ __launch_bounds__(kExpThreads) void k_expand(
+    const DevKey* __restrict__ K, const uint4* __restrict__ in_s, const uint32_t* __restrict__ in_t,
+    int L0, int k, int tile, uint4* __restrict__ out_s, uint32_t* __restrict__ out_t,
+    uint8_t* __restrict__ c) {
+  constexpr int NW = NRP <= 4 ? 1 : NRP / 4;
+  __shared__ ExpSmem sm;
+  load_tables(sm.tab);
+  const Tab T{reinterpret_cast<const char*>(sm.tab), (threadIdx.x & 31u) * 4u};
+  const Bits B(K->p);
+  const uint64_t ibase = (uint64_t)blockIdx.x * tile;
+  const uint64_t obase = ibase << k;
+  uint4 qm;  // keep the nq output bytes
   {
+    const int nq = (int)K->nq;
     uint32_t m[4];
     for (int w = 0; w < 4; ++w) {
-      const int lo = 4 * w;
-      const int nb = (int)nq - lo;
+      const int nb = nq - 4 * w;
       m[w] = nb >= 4 ? 0xffffffffu : (nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u));
     }
-    qmask = make_uint4(m[0], m[1], m[2], m[3]);
+    qm = make_uint4(m[0], m[1], m[2], m[3]);
   }
-  const uint64_t lbase = fbase << d;
-  for (int i = threadIdx.x; i < W; i += blockDim.x) {
-    uint4 o = aes_ctr_block(T, sm.s[cur][i], 0u);
-    const uint32_t t = sm.t[cur][i];
-    for (uint32_t j = 0; j < pm1; ++j) o = xor4(o, and4(K->lastcw[j], 0u - ((t >> j) & 1u)));
-    o = make_uint4(o.x & qmask.x, o.y & qmask.y, o.z & qmask.z, o.w & qmask.w);
-    uint8_t* dst = c + (lbase + i) * NRP;
-    if constexpr (NRP == 1) {
-      *dst = (uint8_t)o.x;
-    } else if constexpr (NRP == 2) {
-      *reinterpret_cast<uint16_t*>(dst) = (uint16_t)o.x;
-    } else if constexpr (NRP == 4) {
-      *reinterpret_cast<uint32_t*>(dst) = o.x;
-    } else if constexpr (NRP == 8) {
-      *reinterpret_cast<uint2*>(dst) = make_uint2(o.x, o.y);
+  if (k == 0) {  // FINAL only: the input nodes are the leaves
+    __syncthreads();
+    for (int i = threadIdx.x; i < tile; i += blockDim.x) {
+      const uint4 v = leaf_value<NW>(T, K, B.pm1, in_s[ibase + i], in_t[ibase + i]);
+      store_leaf<NRP>(c, obase + i, make_uint4(v.x & qm.x, v.y & qm.y, v.z & qm.z, v.w & qm.w));
+    }
+    return;
+  }
+  // level i (width tile << i) lives in buffer a when (k-1-i) is even, else b
+  int buf = (k - 1) & 1;  // buffer of level 0: 0 = a, 1 = b
+  {
+    uint4* s0 = buf ? sm.sb : sm.sa;
+    uint32_t* t0 = buf ? sm.tb : sm.ta;
+    for (int i = threadIdx.x; i < tile; i += blockDim.x) {
+      s0[i] = in_s[ibase + i];
+      t0[i] = in_t[ibase + i];
+    }
+  }
+  __syncthreads();
+  int W = tile;
+  for (int lv = 0; lv < k - 1; ++lv) {
+    const uint4* is = buf ? sm.sb : sm.sa;
+    const uint32_t* it = buf ? sm.tb : sm.ta;
+    uint4* os = buf ? sm.sa : sm.sb;
+    uint32_t* ot = buf ? sm.ta : sm.tb;
+    for (int u = threadIdx.x; u < W; u += blockDim.x) {
+      uint4 sl, sr;
+      uint32_t tl, tr;
+      expand_node(T, K, L0 + lv, B, is[u], it[u], sl, sr, tl, tr);
+      os[2 * u] = sl; os[2 * u + 1] = sr;
+      ot[2 * u] = tl; ot[2 * u + 1] = tr;
+    }
+    __syncthreads();
+    buf ^= 1;
+    W *= 2;
+  }
+  const int L = L0 + k - 1;
+  const uint4* is = buf ? sm.sb : sm.sa;
+  const uint32_t* it = buf ? sm.tb : sm.ta;
+  for (int u = threadIdx.x; u < W; u += blockDim.x) {
+    uint4 sl, sr;
+    uint32_t tl, tr;
+    expand_node(T, K, L, B, is[u], it[u], sl, sr, tl, tr);
+    if constexpr (FINAL) {
+      const uint4 vl = leaf_value<NW>(T, K, B.pm1, sl, tl);
+      const uint4 vr = leaf_value<NW>(T, K, B.pm1, sr, tr);
+      if constexpr (NRP == 1) {  // both leaves in one 16-bit store
+        *reinterpret_cast<uint16_t*>(c + obase + 2 * u) =
+            (uint16_t)((vl.x & qm.x & 0xffu) | ((vr.x & qm.x & 0xffu) << 8));
+      } else {
+        store_leaf<NRP>(c, obase + 2 * u, make_uint4(vl.x & qm.x, vl.y & qm.y, vl.z & qm.z, vl.w & qm.w));
+        store_leaf<NRP>(c, obase + 2 * u + 1, make_uint4(vr.x & qm.x, vr.y & qm.y, vr.z & qm.z, vr.w & qm.w));
+      }
     } else {
-      *reinterpret_cast<uint4*>(dst) = o;
+      out_s[obase + 2 * u] = sl;
+      out_s[obase + 2 * u + 1] = sr;
+      out_t[obase + 2 * u] = tl;
+      out_t[obase + 2 * u + 1] = tr;
     }
   }
 }
@@ -482,50 +574,93 @@ TreePlan make_plan(int n, int log_parts, uint64_t prefix) {
   pl.log_parts = log_parts;
   pl.prefix = prefix;
   const int nr = n - log_parts;  // depth of this partition's subtree
-  pl.d = std::min(nr, 3);
-  const int F = nr - pl.d;       // frontier depth below the partition root
-  // frontier kernel: 2^g workgroups (about two per CU), each expanding e <= 11 levels
-  int g = std::min(F, 9);
-  if (F - g > 11) g = F - 11;
-  pl.g = g;
-  pl.e = F - g;
-  pl.nfront = 1ull << F;
-  pl.tile = (int)std::min<uint64_t>(pl.nfront, (uint64_t)(kNodeCap >> pl.d));
   pl.nleaves = 1ull << nr;
+  // frontier (latency-bound, column-shape AES) down to F, then row-shape stages of <= 4
+  // levels each, the last one fused with the leaf conversion
+  const int F = nr <= 4 ? 0 : std::min(16, nr - 4);
+  pl.F = F;
+  pl.g = std::min(F, 8);
+  pl.e = F - pl.g;
+  pl.nfront = 1ull << F;
+  int rem = nr - F, L = log_parts + F;
+  uint64_t nin = pl.nfront;
+  int ks[8], ns = 0;
+  if (rem == 0) {
+    ks[ns++] = 0;
+  } else {
+    while (rem > 0) {
+      const int k = rem % 4 ? rem % 4 : 4;  // remainder first, then full 4-level stages
+      ks[ns++] = k;
+      rem -= k;
+    }
+  }
+  uint64_t maxnodes = pl.nfront;
+  for (int i = 0; i < ns; ++i) {
+    Stage& st = pl.st[i];
+    st.L_in = L;
+    st.k = ks[i];
+    st.nin = nin;
+    st.tile = (int)std::min<uint64_t>(nin, (uint64_t)(kExpOut >> st.k));
+    st.final = i == ns - 1;
+    L += st.k;
+    nin <<= st.k;
+    if (!st.final) maxnodes = std::max(maxnodes, nin);
+  }
+  pl.nstages = ns;
+  pl.max_nodes = maxnodes;
   return pl;
 }
 
-hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys, int p, int n,
-                           int nq, int party0, DevKey* d_keys, hipStream_t s) {
-  hipLaunchKernelGGL(k_key_prep, dim3(num_keys), dim3(256), 0, s, d_raw, key_stride, p, n, nq,
-                     party0, d_keys);
+hipError_t launch_frontier(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_frontier, dim3(1u << pl.g), dim3(kFrontThreads), 0, s, d_key, pl.prefix,
+                     pl.log_parts, pl.g, pl.e, nb.s[0], nb.t[0]);
   return hipGetLastError();
 }
 
-hipError_t launch_frontier(const TreePlan& pl, const DevKey* d_key, uint4* d_front_s,
-                           uint32_t* d_front_t, hipStream_t s) {
-  hipLaunchKernelGGL(k_tree_frontier, dim3(1u << pl.g), dim3(kTreeThreads), 0, s, d_key,
-                     pl.prefix, pl.log_parts, pl.g, pl.e, d_front_s, d_front_t);
+template <int NRP>
+static hipError_t launch_stage(const Stage& st, const DevKey* d_key, const uint4* is,
+                               const uint32_t* it, uint4* os, uint32_t* ot, uint8_t* c,
+                               unsigned blocks, hipStream_t s) {
+  if (st.final)
+    hipLaunchKernelGGL((k_expand<true, NRP>), dim3(blocks), dim3(kExpThreads), 0, s, d_key, is,
+                       it, st.L_in, st.k, st.tile, os, ot, c);
+  else
+    hipLaunchKernelGGL((k_expand<false, 1>), dim3(blocks), dim3(kExpThreads), 0, s, d_key, is,
+                       it, st.L_in, st.k, st.tile, os, ot, c);
   return hipGetLastError();
 }
 
-hipError_t launch_leaves(const TreePlan& pl, const DevKey* d_key, const uint4* d_front_s,
-                         const uint32_t* d_front_t, uint64_t f0, uint64_t nf, uint8_t* d_c,
-                         int nrp, hipStream_t s) {
-  const int L0 = pl.log_parts + pl.g + pl.e;
-  const dim3 grid((unsigned)(nf / pl.tile));
-  const uint4* fs = d_front_s + f0;
-  const uint32_t* ft = d_front_t + f0;
-  uint8_t* c = d_c + (f0 << pl.d) * nrp;
-  switch (nrp) {
-    case 1: hipLaunchKernelGGL(k_tree_leaves<1>, grid, dim3(kTreeThreads), 0, s, d_key, fs, ft, L0, pl.d, pl.tile, c); break;
-    case 2: hipLaunchKernelGGL(k_tree_leaves<2>, grid, dim3(kTreeThreads), 0, s, d_key, fs, ft, L0, pl.d, pl.tile, c); break;
-    case 4: hipLaunchKernelGGL(k_tree_leaves<4>, grid, dim3(kTreeThreads), 0, s, d_key, fs, ft, L0, pl.d, pl.tile, c); break;
-    case 8: hipLaunchKernelGGL(k_tree_leaves<8>, grid, dim3(kTreeThreads), 0, s, d_key, fs, ft, L0, pl.d, pl.tile, c); break;
-    case 16: hipLaunchKernelGGL(k_tree_leaves<16>, grid, dim3(kTreeThreads), 0, s, d_key, fs, ft, L0, pl.d, pl.tile, c); break;
-    default: return hipErrorInvalidValue;
+// stages of chunk j of C (each stage's input range split evenly); c rows of the chunk's leaves
+hipError_t launch_stages(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb, int j, int C,
+                         uint8_t* d_c, int nrp, hipStream_t s) {
+  for (int i = 0; i < pl.nstages; ++i) {
+    const Stage& st = pl.st[i];
+    const uint64_t nin = st.nin / C, i0 = nin * j, o0 = i0 << st.k;
+    const uint4* is = nb.s[i & 1] + i0;
+    const uint32_t* it = nb.t[i & 1] + i0;
+    uint4* os = nb.s[(i + 1) & 1] + o0;
+    uint32_t* ot = nb.t[(i + 1) & 1] + o0;
+    uint8_t* c = d_c + o0 * nrp;
+    const unsigned blocks = (unsigned)(nin / st.tile);
+    hipError_t e;
+    switch (nrp) {
+      case 1: e = launch_stage<1>(st, d_key, is, it, os, ot, c, blocks, s); break;
+      case 2: e = launch_stage<2>(st, d_key, is, it, os, ot, c, blocks, s); break;
+      case 4: e = launch_stage<4>(st, d_key, is, it, os, ot, c, blocks, s); break;
+      case 8: e = launch_stage<8>(st, d_key, is, it, os, ot, c, blocks, s); break;
+      case 16: e = launch_stage<16>(st, d_key, is, it, os, ot, c, blocks, s); break;
+      default: return hipErrorInvalidValue;
+    }
+    if (e != hipSuccess) return e;
   }
-  return hipGetLastError();
+  return hipSuccess;
+}
+
+int max_chunks(const TreePlan& pl) {  // C must divide every stage's workgroup count
+  uint64_t c = 1ull << 20;
+  for (int i = 0; i < pl.nstages; ++i) c = std::min<uint64_t>(c, pl.st[i].nin / pl.st[i].tile);
+  return (int)c;
 }
 
 static int vec_for(int nq) { return nq <= 2 ? 4 : (nq <= 8 ? 2 : 1); }
