@@ -611,6 +611,13 @@ TreePlan make_plan(int n, int log_parts, uint64_t prefix) {
   return pl;
 }
 
+hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys, int p, int n,
+                           int nq, int party0, DevKey* d_keys, hipStream_t s) {
+  hipLaunchKernelGGL(k_key_prep, dim3(num_keys), dim3(256), 0, s, d_raw, key_stride, p, n, nq,
+                     party0, d_keys);
+  return hipGetLastError();
+}
+
 hipError_t launch_frontier(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb,
                            hipStream_t s) {
   hipLaunchKernelGGL(k_frontier, dim3(1u << pl.g), dim3(kFrontThreads), 0, s, d_key, pl.prefix,

@@ -12,6 +12,7 @@ step() {  # name timeout cmd...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
   return $rc
 }
+python -c "import erasurecodedpir_amd as p; p.load()" || { echo "library does not load"; exit 3; }
 [ -n "$SKIP_TESTS" ] || step pytest_gpu 900 python -m pytest tests -m gpu -x -q
 step bench_c2 300 python bench.py --steps 50 --warmup 5
 [ -n "$SKIP_C24" ] || step bench_c24 300 python bench.py --config c24 --steps 20 --warmup 3 --no-cpu
