@@ -173,6 +173,7 @@ def main():
     dt_prof = timed(args.steps)
     phases = eng.last_timings()
     eng.set_profiling(0)
+    alone = eng.profile_phases(d_key, 10)
     gpu_answer = eng.d2h(d_res, eng.answer_bytes).reshape(nq, efs)
 
     # PIR correctness at full size (every rank): party-1 ^ party-2 answers == finalCW * record
@@ -238,6 +239,7 @@ def main():
             "scan_ms_per_launch": round(scan_ms / chunks, 5),
         },
         "phases_ms": {k: round(v, 5) for k, v in phases.items() if k != "chunks"},
+        "phases_alone_ms": {k: round(v, 5) for k, v in alone.items()},
         "instrumented_ms_per_step": round(dt_prof / args.steps * 1e3, 5),
         "inclusive_h2d_key_d2h_answer": {"ms_per_query": round(incl_ms, 4),
                                          "value": round(shard_bytes / GIB / (incl_ms / 1e3), 3),

@@ -135,11 +135,11 @@ int ensure_slabs(pir_engine* e, size_t bytes) {
   return PIR_OK;
 }
 
-int pick_chunks(const pir::TreePlan& pl) {
-  // pipeline only when every chunk still fills the GPU (>= 2^16 records)
-  const int cmax = std::min(kMaxChunks, pir::max_chunks(pl));
+int pick_chunks(const pir::TreePlan& pl, int num_cus) {
+  // pipeline the leaf stage only while each chunk's launch still covers every CU
+  const int blocks = pir::final_stage_blocks(pl);
   int c = 1;
-  while (2 * c <= cmax && (pl.nleaves >> 16) >= (uint64_t)(2 * c)) c *= 2;
+  while (2 * c <= kMaxChunks && blocks % (2 * c) == 0 && blocks / (2 * c) >= num_cus) c *= 2;
   return c;
 }
 
@@ -151,7 +151,7 @@ int answer_core(pir_engine* e, const pir::DevKey* d_key, int log_parts_total, ui
                 uint64_t row0, uint8_t* d_out, hipStream_t s) {
   const auto& c = e->cfg;
   const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix);
-  const int C = pick_chunks(pl);
+  const int C = pick_chunks(pl, e->num_cus);
   e->last_chunks = C;
   const uint64_t nrec = pl.nleaves / C;
   const pir::ScanShape sh = pir::make_scan_shape(nrec, e->pitch, c.num_rounds, e->num_cus);
@@ -160,10 +160,11 @@ int answer_core(pir_engine* e, const pir::DevKey* d_key, int log_parts_total, ui
   hipEvent_t* ev = e->ev;
   if (ev) HIP_TRY(hipEventRecord(ev[EV_KEY], s));
   HIP_TRY(pir::launch_frontier(pl, d_key, e->nodes, s));
+  HIP_TRY(pir::launch_stages(pl, d_key, e->nodes, 0, 1, e->d_c, e->nrp, s, 0, pl.nstages - 1));
   if (ev) HIP_TRY(hipEventRecord(ev[EV_FRONT], s));
   for (int j = 0; j < C; ++j) {
     if (ev) HIP_TRY(hipEventRecord(ev[EV_LEAF_B + j], s));
-    HIP_TRY(pir::launch_stages(pl, d_key, e->nodes, j, C, e->d_c, e->nrp, s));
+    HIP_TRY(pir::launch_stages(pl, d_key, e->nodes, j, C, e->d_c, e->nrp, s, pl.nstages - 1));
     if (ev) HIP_TRY(hipEventRecord(ev[EV_LEAF_E + j], s));
     HIP_TRY(hipEventRecord(e->ev_leaf[j], s));
     HIP_TRY(hipStreamWaitEvent(e->aux, e->ev_leaf[j], 0));
@@ -559,6 +560,44 @@ int pir_engine_last_timings(pir_engine_t* e, pir_kernel_time* out, int max) {
   std::lock_guard<std::mutex> lk(e->mu);
   HIP_TRY(hipSetDevice(e->cfg.device));
   return read_timings(e, out, max);
+}
+
+int pir_engine_profile_phases(pir_engine_t* e, const uint8_t* d_key, int iters, float* out_ms) {
+  if (!e || !d_key || !out_ms || iters < 1) return fail(PIR_EINVAL, "bad argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  const auto& c = e->cfg;
+  HIP_TRY(hipSetDevice(c.device));
+  hipStream_t s = e->stream;
+  const pir::TreePlan pl =
+      pir::make_plan(c.log_num_records, c.log_num_partitions, (uint64_t)c.partition_index);
+  const pir::ScanShape sh = pir::make_scan_shape(pl.nleaves, e->pitch, c.num_rounds, e->num_cus);
+  int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
+  if (rc) return rc;
+  hipEvent_t ev[6];
+  for (auto& x : ev) HIP_TRY(hipEventCreate(&x));
+  HIP_TRY(hipEventRecord(ev[0], s));
+  for (int i = 0; i < iters; ++i)
+    HIP_TRY(pir::launch_key_prep(d_key, e->key_len, 1, c.num_parties, c.log_num_records,
+                                 c.num_rounds, c.party_index - 1, e->d_keys, s));
+  HIP_TRY(hipEventRecord(ev[1], s));
+  for (int i = 0; i < iters; ++i) HIP_TRY(pir::launch_frontier(pl, e->d_keys, e->nodes, s));
+  HIP_TRY(hipEventRecord(ev[2], s));
+  for (int i = 0; i < iters; ++i)
+    HIP_TRY(pir::launch_stages(pl, e->d_keys, e->nodes, 0, 1, e->d_c, e->nrp, s));
+  HIP_TRY(hipEventRecord(ev[3], s));
+  for (int i = 0; i < iters; ++i)
+    HIP_TRY(pir::launch_scan(sh, e->d_shard, pl.nleaves, e->d_c, e->d_slabs, false, s));
+  HIP_TRY(hipEventRecord(ev[4], s));
+  for (int i = 0; i < iters; ++i) HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, e->d_result, s));
+  HIP_TRY(hipEventRecord(ev[5], s));
+  HIP_TRY(hipEventSynchronize(ev[5]));
+  for (int i = 0; i < 5; ++i) {
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+    out_ms[i] = ms / iters;
+  }
+  for (auto& x : ev) (void)hipEventDestroy(x);
+  return PIR_OK;
 }
 
 int pir_engine_get_shard(pir_engine_t* e, uint64_t row0, uint64_t nrows, uint8_t* out) {

@@ -48,7 +48,7 @@ struct NodeBufs {  // ping-pong node arrays in global memory (max_nodes entries 
 };
 
 TreePlan make_plan(int n, int log_parts, uint64_t prefix);
-int max_chunks(const TreePlan& pl);
+int final_stage_blocks(const TreePlan& pl);  // workgroups of the leaf-converting stage
 
 void upload_aes_table(hipStream_t s);  // Te0 (computed on the host) -> __constant__ memory
 
@@ -56,9 +56,9 @@ hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys
                            int nq, int party0, DevKey* d_keys, hipStream_t s);
 hipError_t launch_frontier(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb,
                            hipStream_t s);
-// the expand stages of chunk j of C -> c rows of that chunk's leaves
+// expand stages [i0, i1) (i1 < 0: to the last) for chunk j of C of every stage's input range
 hipError_t launch_stages(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb, int j, int C,
-                         uint8_t* d_c, int nrp, hipStream_t s);
+                         uint8_t* d_c, int nrp, hipStream_t s, int i0 = 0, int i1 = -1);
 // scan rows [0, nrec) of `shard` (row pitch `pitch`) with coefficients cT[i*nrp + a]
 struct ScanShape {
   int nq, nrp, vec;      // vec = dwords per lane chunk (4, 2, 1)

@@ -638,10 +638,11 @@ static hipError_t launch_stage(const Stage& st, const DevKey* d_key, const uint4
   return hipGetLastError();
 }
 
-// stages of chunk j of C (each stage's input range split evenly); c rows of the chunk's leaves
+// stages [i0, i1) of chunk j of C (each stage's input range split evenly)
 hipError_t launch_stages(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb, int j, int C,
-                         uint8_t* d_c, int nrp, hipStream_t s) {
-  for (int i = 0; i < pl.nstages; ++i) {
+                         uint8_t* d_c, int nrp, hipStream_t s, int i0s, int i1s) {
+  if (i1s < 0) i1s = pl.nstages;
+  for (int i = i0s; i < i1s; ++i) {
     const Stage& st = pl.st[i];
     const uint64_t nin = st.nin / C, i0 = nin * j, o0 = i0 << st.k;
     const uint4* is = nb.s[i & 1] + i0;
@@ -664,10 +665,9 @@ hipError_t launch_stages(const TreePlan& pl, const DevKey* d_key, const NodeBufs
   return hipSuccess;
 }
 
-int max_chunks(const TreePlan& pl) {  // C must divide every stage's workgroup count
-  uint64_t c = 1ull << 20;
-  for (int i = 0; i < pl.nstages; ++i) c = std::min<uint64_t>(c, pl.st[i].nin / pl.st[i].tile);
-  return (int)c;
+int final_stage_blocks(const TreePlan& pl) {
+  const Stage& st = pl.st[pl.nstages - 1];
+  return (int)(st.nin / st.tile);
 }
 
 static int vec_for(int nq) { return nq <= 2 ? 4 : (nq <= 8 ? 2 : 1); }

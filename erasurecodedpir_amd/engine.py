@@ -165,6 +165,13 @@ class Engine:
             check(n, "last_timings")
         return {arr[i].name.decode(): float(arr[i].ms) for i in range(n)}
 
+    def profile_phases(self, d_key, iters=10):
+        """Each phase alone (diagnostics): {phase: mean ms}."""
+        out = (ctypes.c_float * 5)()
+        check(self._lib.pir_engine_profile_phases(self._h, d_key, iters, out), "profile_phases")
+        names = ["key_prep", "tree_frontier", "tree_stages", "scan", "reduce"]
+        return {n: float(out[i]) for i, n in enumerate(names)}
+
     # -- split shard ---------------------------------------------------------------------------
     def attach_comm(self, unique_id, nranks, rank):
         uid, up = _buf(unique_id)

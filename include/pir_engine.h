@@ -106,6 +106,10 @@ typedef struct {
 } pir_kernel_time;
 int pir_engine_set_profiling(pir_engine_t *e, int slots);
 int pir_engine_last_timings(pir_engine_t *e, pir_kernel_time *out, int max);
+/* diagnostics: each phase run alone `iters` times back to back (no pipelining); out_ms[5] =
+ * mean ms of key_prep, tree_frontier, tree_stages (all expand stages), scan (one launch over
+ * all rows), reduce.  d_key: device pointer to one raw key. */
+int pir_engine_profile_phases(pir_engine_t *e, const uint8_t *d_key, int iters, float *out_ms);
 
 /* ---- split shard across GPUs: XOR all-reduce of partition answers over RCCL ---- */
 #define PIR_COMM_ID_BYTES 128
