@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -84,6 +85,8 @@ struct pir_engine {
   hipEvent_t ev_leaf[kMaxChunks] = {};    // leaves of chunk j written
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int last_chunks = 1;
+  int last_fused = 0;
+  bool allow_fused = true;  // $PIR_FUSED=0 forces the 2-kernel path (A/B diagnostics)
   uint8_t* d_shard = nullptr;
   uint8_t* d_key_raw = nullptr;  // max_batch keys
   pir::DevKey* d_keys = nullptr; // max_batch parsed keys
@@ -147,9 +150,45 @@ int pick_chunks(const pir::TreePlan& pl, int num_cus) {
 // with the tree rooted at `prefix` (depth log_parts_total).  d_key points at ONE parsed key.
 //   s  : key prep, frontier, leaves(0..C-1), [join], reduce
 //   aux: scan(j) after leaves(j)  -- so leaves(j+1) overlaps scan(j)
+int answer_fused(pir_engine* e, const pir::DevKey* d_key, int log_parts_total, uint64_t prefix,
+                 uint64_t row0, uint8_t* d_out, hipStream_t s, int tile) {
+  const auto& c = e->cfg;
+  const pir::TreePlan pl =
+      pir::make_plan(c.log_num_records, log_parts_total, prefix, pir::fused_k(tile));
+  const pir::ScanShape sh =
+      pir::make_fused_shape(pl.nleaves, e->pitch, c.num_rounds, e->num_cus, tile);
+  int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
+  if (rc) return rc;
+  e->last_chunks = 1;
+  e->last_fused = 1;
+  hipEvent_t* ev = e->ev;
+  if (ev) HIP_TRY(hipEventRecord(ev[EV_KEY], s));
+  HIP_TRY(pir::launch_frontier(pl, d_key, e->nodes, s));
+  HIP_TRY(pir::launch_stages(pl, d_key, e->nodes, 0, 1, e->d_c, e->nrp, s, 0, pl.nstages - 1));
+  if (ev) {
+    HIP_TRY(hipEventRecord(ev[EV_FRONT], s));
+    HIP_TRY(hipEventRecord(ev[EV_LEAF_B], s));
+    HIP_TRY(hipEventRecord(ev[EV_LEAF_E], s));
+    HIP_TRY(hipEventRecord(ev[EV_SCAN_B], s));
+  }
+  HIP_TRY(pir::launch_fused(pl, d_key, e->nodes, e->d_shard + row0 * e->pitch, sh, e->d_slabs,
+                            tile, s));
+  if (ev) {
+    HIP_TRY(hipEventRecord(ev[EV_SCAN_E], s));
+    HIP_TRY(hipEventRecord(ev[EV_PRERED], s));
+  }
+  HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, d_out, s));
+  if (ev) HIP_TRY(hipEventRecord(ev[EV_RED], s));
+  return PIR_OK;
+}
+
 int answer_core(pir_engine* e, const pir::DevKey* d_key, int log_parts_total, uint64_t prefix,
                 uint64_t row0, uint8_t* d_out, hipStream_t s) {
   const auto& c = e->cfg;
+  const uint64_t nleaves = 1ull << (c.log_num_records - log_parts_total);
+  const int tile = e->allow_fused ? pir::fused_tile(c.num_rounds, e->pitch, nleaves, e->num_cus) : 0;
+  if (tile) return answer_fused(e, d_key, log_parts_total, prefix, row0, d_out, s, tile);
+  e->last_fused = 0;
   const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix);
   const int C = pick_chunks(pl, e->num_cus);
   e->last_chunks = C;
@@ -184,8 +223,8 @@ int answer_core(pir_engine* e, const pir::DevKey* d_key, int log_parts_total, ui
 int check_key_ptr(const void* p) { return p ? PIR_OK : fail(PIR_EINVAL, "null key"); }
 
 const char* const kPhaseNames[] = {"key_prep", "tree_frontier", "tree_leaves", "scan",
-                                   "reduce", "comm_fold", "total", "chunks"};
-constexpr int kNumPhases = 8;
+                                   "reduce", "comm_fold", "total", "chunks", "fused"};
+constexpr int kNumPhases = 9;
 
 // Mean per-phase device times over the answers recorded since the last read.  tree_leaves and
 // scan are the summed kernel durations of the C pipelined chunks (they overlap each other).
@@ -214,6 +253,7 @@ int read_timings(pir_engine* e, pir_kernel_time* out, int max) {
     HIP_TRY(el(v[EV_START], v[EV_END], acc[6]));
   }
   acc[7] = C * cnt;
+  acc[8] = e->last_fused * cnt;
   for (int i = 0; i < n; ++i) {
     snprintf(out[i].name, sizeof out[i].name, "%s", kPhaseNames[i]);
     out[i].ms = (float)(acc[i] / cnt);
@@ -310,7 +350,17 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
     return cleanup(fail(PIR_ENOMEM, "hipMalloc shard %zu bytes", shard_bytes));
   if (hipMemsetAsync(e->d_shard, 0, shard_bytes, e->stream) != hipSuccess)
     return cleanup(fail(PIR_EHIP, "hipMemset shard"));
-  const pir::TreePlan pl = pir::make_plan(c.log_num_records, c.log_num_partitions, 0);
+  pir::TreePlan pl = pir::make_plan(c.log_num_records, c.log_num_partitions, 0);
+  {
+    const char* f = getenv("PIR_FUSED");
+    e->allow_fused = !(f && f[0] == '0');
+    const int tile = pir::fused_tile(c.num_rounds, e->pitch, e->rows, e->num_cus);
+    if (tile) {
+      const pir::TreePlan pf =
+          pir::make_plan(c.log_num_records, c.log_num_partitions, 0, pir::fused_k(tile));
+      if (pf.max_nodes > pl.max_nodes) pl = pf;
+    }
+  }
   const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
   if (hipMalloc(&e->nodes.s[0], pl.max_nodes * sizeof(uint4)) != hipSuccess ||
       hipMalloc(&e->nodes.s[1], pl.max_nodes * sizeof(uint4)) != hipSuccess ||

@@ -47,7 +47,8 @@ struct NodeBufs {  // ping-pong node arrays in global memory (max_nodes entries 
   uint32_t* t[2];
 };
 
-TreePlan make_plan(int n, int log_parts, uint64_t prefix);
+// k_last: levels of the leaf-converting last stage (-1: default 4 for k_expand<FINAL>)
+TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last = -1);
 int final_stage_blocks(const TreePlan& pl);  // workgroups of the leaf-converting stage
 
 void upload_aes_table(hipStream_t s);  // Te0 (computed on the host) -> __constant__ memory
@@ -71,6 +72,14 @@ ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus);
 // accumulate: XOR into the slabs instead of overwriting them (chunked scans of one answer)
 hipError_t launch_scan(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
                        const uint8_t* d_c, uint8_t* d_slabs, bool accumulate, hipStream_t s);
+// Fused leaf stage + scan (one persistent workgroup per CU).  fused_tile() = leaves per tile
+// (0: not supported for this shape -> 2-kernel path); plan with make_plan(.., fused_k(tile)).
+int fused_tile(int nq, uint32_t pitch, uint64_t nleaves, int num_cus);
+int fused_k(int tile);
+ScanShape make_fused_shape(uint64_t nleaves, uint32_t pitch, int nq, int num_cus, int tile);
+hipError_t launch_fused(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb,
+                        const uint8_t* shard, const ScanShape& sh, uint8_t* slabs, int tile,
+                        hipStream_t s);
 // XOR the slabs, compact pitch -> record_bytes: d_out[a*efs + b]
 hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t efs,
                          uint8_t* d_out, hipStream_t s);

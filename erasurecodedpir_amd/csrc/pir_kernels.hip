@@ -479,6 +479,230 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
     for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) slab[i] = red[i];
 }
 
+// ------------------------------------------------------------------------------------------
+// k_fused: the leaf stage of the tree and the shard scan in ONE persistent kernel, one
+// workgroup per CU, waves specialised by role so the AES tree (VALU + LDS bound) runs under
+// the HBM-bound scan on every CU:
+//   tree waves [0, TW)   : tile i (TILE_LEAVES leaves) = expand `tile_in` nodes of level L_in
+//                          by k levels (row-shape AES, breadth-first in LDS, synchronised by an
+//                          LDS counter barrier among the tree waves only) and write the DPF
+//                          shares c[leaf][0..NRP) into LDS ring slot i % 2;
+//   scan waves [TW, 16)  : stream the shard rows of tile i from HBM and fold them into the
+//                          per-lane GF(2^8) bit-plane accumulators with the shares of slot i%2.
+// Handshake through two LDS counters: `ready` (tiles produced) and `consumed` (scan-wave
+// arrivals), so the tree can run one tile ahead.  The shares never leave the CU.
+// ------------------------------------------------------------------------------------------
+constexpr int kFusedThreads = 1024;
+constexpr int kFusedWaves = kFusedThreads / 64;
+
+template <int TILE, int NRP, int NQ, int VEC, int GYMAX>
+struct FusedSmem {
+  uint32_t tab[2 * 256 * 32];
+  uint4 sa[TILE / 2];
+  uint32_t ta[TILE / 2];
+  uint4 sb[TILE / 4];
+  uint32_t tb[TILE / 4];
+  uint8_t ring[2][TILE * NRP];
+  uint32_t red[GYMAX][NQ * kColGroupLanes * VEC];
+  uint32_t bar, ready, consumed;
+};
+
+__device__ __forceinline__ uint32_t lds_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_geq(const uint32_t* p, uint32_t v) {
+  while (lds_load(p) < v) __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ void lds_signal(uint32_t* p) {  // one lane per wave
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// barrier among `nw` waves (not the whole workgroup): generation-counted LDS counter
+__device__ __forceinline__ void group_barrier(uint32_t* ctr, uint32_t& gen, uint32_t nw) {
+  lds_signal(ctr);
+  gen += nw;
+  lds_wait_geq(ctr, gen);
+}
+
+template <int NQ, int NRP, int VEC, bool UNI, int TW, int TILE, int GYMAX>
+__global__ __launch_bounds__(kFusedThreads) void k_fused(
+    const DevKey* __restrict__ K, const uint4* __restrict__ in_s, const uint32_t* __restrict__ in_t,
+    int L_in, int k, uint64_t ntiles, const uint8_t* __restrict__ shard, uint32_t pitch,
+    uint32_t cpr, uint32_t gy, uint8_t* __restrict__ slabs) {
+  constexpr int SW = kFusedWaves - TW;
+  constexpr int CH = VEC * 4;
+  constexpr int GW = kColGroupLanes * VEC;
+  constexpr int NW = NRP <= 4 ? 1 : NRP / 4;
+  using Smem = FusedSmem<TILE, NRP, NQ, VEC, GYMAX>;
+  __shared__ Smem sm;
+  load_tables(sm.tab);
+  for (int i = threadIdx.x; i < GYMAX * NQ * GW; i += blockDim.x) (&sm.red[0][0])[i] = 0;
+  if (threadIdx.x == 0) { sm.bar = 0; sm.ready = 0; sm.consumed = 0; }
+  __syncthreads();
+
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t G = gridDim.x, b = blockIdx.x;
+  const uint32_t my_tiles = ntiles > b ? (uint32_t)((ntiles - 1 - b) / G + 1) : 0u;
+  const int tile_in = TILE >> k;
+
+  if (wave < (uint32_t)TW) {
+    // ===================================== tree role ======================================
+    const Tab T{reinterpret_cast<const char*>(sm.tab), (threadIdx.x & 31u) * 4u};
+    const Bits B(K->p);
+    const int tt = threadIdx.x, nt = TW * 64;
+    uint32_t gen = 0;
+    uint4 qm;
+    {
+      const int nq = (int)K->nq;
+      uint32_t m[4];
+      for (int w = 0; w < 4; ++w) {
+        const int nb = nq - 4 * w;
+        m[w] = nb >= 4 ? 0xffffffffu : (nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u));
+      }
+      qm = make_uint4(m[0], m[1], m[2], m[3]);
+    }
+    for (uint32_t i = 0; i < my_tiles; ++i) {
+      const uint64_t tile = b + (uint64_t)i * G;
+      const uint64_t ibase = tile * tile_in;
+      uint8_t* ring = sm.ring[i & 1];
+      if (i >= 2) lds_wait_geq(&sm.consumed, (i - 1) * SW);  // slot free: tile i-2 scanned
+      int buf = (k - 1) & 1;
+      {
+        uint4* s0 = buf ? sm.sb : sm.sa;
+        uint32_t* t0 = buf ? sm.tb : sm.ta;
+        for (int u = tt; u < tile_in; u += nt) {
+          s0[u] = in_s[ibase + u];
+          t0[u] = in_t[ibase + u];
+        }
+      }
+      group_barrier(&sm.bar, gen, TW);
+      int W = tile_in;
+      for (int lv = 0; lv < k - 1; ++lv) {
+        const uint4* is = buf ? sm.sb : sm.sa;
+        const uint32_t* it = buf ? sm.tb : sm.ta;
+        uint4* os = buf ? sm.sa : sm.sb;
+        uint32_t* ot = buf ? sm.ta : sm.tb;
+        for (int u = tt; u < W; u += nt) {
+          uint4 sl, sr;
+          uint32_t tl, tr;
+          expand_node(T, K, L_in + lv, B, is[u], it[u], sl, sr, tl, tr);
+          os[2 * u] = sl; os[2 * u + 1] = sr;
+          ot[2 * u] = tl; ot[2 * u + 1] = tr;
+        }
+        group_barrier(&sm.bar, gen, TW);
+        buf ^= 1;
+        W *= 2;
+      }
+      {
+        const uint4* is = buf ? sm.sb : sm.sa;
+        const uint32_t* it = buf ? sm.tb : sm.ta;
+        const int L = L_in + k - 1;
+        for (int u = tt; u < W; u += nt) {
+          uint4 sl, sr;
+          uint32_t tl, tr;
+          expand_node(T, K, L, B, is[u], it[u], sl, sr, tl, tr);
+          uint4 vl = leaf_value<NW>(T, K, B.pm1, sl, tl);
+          uint4 vr = leaf_value<NW>(T, K, B.pm1, sr, tr);
+          vl = make_uint4(vl.x & qm.x, vl.y & qm.y, vl.z & qm.z, vl.w & qm.w);
+          vr = make_uint4(vr.x & qm.x, vr.y & qm.y, vr.z & qm.z, vr.w & qm.w);
+          if constexpr (NRP == 1) {
+            *reinterpret_cast<uint16_t*>(ring + 2 * u) = (uint16_t)((vl.x & 0xffu) | ((vr.x & 0xffu) << 8));
+          } else {
+            store_leaf<NRP>(ring, 2 * u, vl);
+            store_leaf<NRP>(ring, 2 * u + 1, vr);
+          }
+        }
+      }
+      group_barrier(&sm.bar, gen, TW);  // every share of tile i is in the ring
+      if (wave == 0) lds_signal(&sm.ready);
+    }
+  } else {
+    // ===================================== scan role ======================================
+    const uint32_t sw = wave - TW;
+    uint32_t gcol, wi, nwg, rpw, rec_off, chunk;
+    bool active;
+    if (UNI) {  // gy column groups share the SW waves
+      gcol = sw % gy;
+      wi = sw / gy;
+      nwg = SW / gy;
+      rpw = 1; rec_off = 0;
+      chunk = gcol * kColGroupLanes + lane;
+      active = chunk < cpr && wi < nwg;
+    } else {
+      gcol = 0; wi = sw; nwg = SW;
+      rpw = kColGroupLanes / cpr;
+      rec_off = lane / cpr;
+      chunk = lane - rec_off * cpr;
+      active = lane < rpw * cpr;
+    }
+    uint32_t Z[NQ][8][VEC];
+#pragma unroll
+    for (int a = 0; a < NQ; ++a)
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) Z[a][kk][v] = 0;
+    const uint32_t ngroups = (TILE + rpw - 1) / rpw;
+    constexpr int U = SW >= 8 ? 8 : 16;
+    for (uint32_t i = 0; i < my_tiles; ++i) {
+      const uint64_t tile = b + (uint64_t)i * G;
+      const uint8_t* ring = sm.ring[i & 1];
+      lds_wait_geq(&sm.ready, i + 1);
+      if (wi < nwg) {
+        const uint8_t* base = shard + (tile * TILE) * pitch + (uint64_t)chunk * CH;
+        // this wave's row groups: wi, wi + nwg, ...  (U rows in flight per lane)
+        for (uint32_t g0 = wi; g0 < ngroups; g0 += U * nwg) {
+          Chunk<VEC> x[U];
+          uint4 cf[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t gi = g0 + u * nwg;
+            const uint32_t rl = gi * rpw + rec_off;
+            const bool ok = active && gi < ngroups && rl < TILE;
+            if (ok) x[u] = load_chunk<VEC>(base + (uint64_t)rl * pitch);
+            else
+              for (int v = 0; v < VEC; ++v) x[u].v[v] = 0;
+            cf[u] = ok ? load_coef<NRP>(ring, rl) : make_uint4(0, 0, 0, 0);
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int a = 0; a < NQ; ++a) {
+              const uint32_t ca = coef_byte(cf[u], a);
+#pragma unroll
+              for (int kk = 0; kk < 8; ++kk) {
+                const uint32_t m = 0u - ((ca >> kk) & 1u);
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= x[u].v[v] & m;
+              }
+            }
+        }
+      }
+      lds_signal(&sm.consumed);
+    }
+    if (active) {
+      const uint32_t wbase = (UNI ? lane : chunk) * VEC;
+#pragma unroll
+      for (int a = 0; a < NQ; ++a)
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          uint32_t acc = Z[a][7][v];
+#pragma unroll
+          for (int kk = 6; kk >= 0; --kk) acc = gf_xtime4(acc) ^ Z[a][kk][v];
+          if (acc) atomicXor(&sm.red[gcol][a * GW + wbase + v], acc);
+        }
+    }
+  }
+  __syncthreads();
+  for (uint32_t g = 0; g < gy; ++g) {
+    uint32_t* slab = reinterpret_cast<uint32_t*>(slabs) + ((uint64_t)g * gridDim.x + blockIdx.x) * (NQ * GW);
+    for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) slab[i] = sm.red[g][i];
+  }
+}
+
 // slabs: [grid.y][grid.x][nq][GW words]; out[a*efs + b] for b < efs.
 // One 1024-thread block per 64 output words: 16 lane groups split the gx slabs, then LDS.
 __global__ __launch_bounds__(kReduceThreads) void k_reduce(const uint32_t* __restrict__ slabs,
@@ -568,39 +792,39 @@ __global__ void k_fill_shard(uint8_t* __restrict__ shard, uint64_t rows, uint32_
 // ------------------------------------------------------------------------------------------
 // host side: tables, plans, launchers
 // ------------------------------------------------------------------------------------------
-TreePlan make_plan(int n, int log_parts, uint64_t prefix) {
+TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last) {
   TreePlan pl{};
   pl.n = n;
   pl.log_parts = log_parts;
   pl.prefix = prefix;
   const int nr = n - log_parts;  // depth of this partition's subtree
   pl.nleaves = 1ull << nr;
-  // frontier (latency-bound, column-shape AES) down to F, then row-shape stages of <= 4
-  // levels each, the last one fused with the leaf conversion
-  const int F = nr <= 4 ? 0 : std::min(16, nr - 4);
+  // frontier (latency-bound, column-shape AES) down to F, row-shape stages of <= 4 levels,
+  // and a last stage of k_last levels that converts the leaves (k_expand<FINAL> or k_fused)
+  if (k_last < 0) k_last = 4;
+  k_last = std::min(k_last, nr);
+  const int L_last = nr - k_last;
+  const int F = std::min(16, L_last);
   pl.F = F;
   pl.g = std::min(F, 8);
   pl.e = F - pl.g;
   pl.nfront = 1ull << F;
-  int rem = nr - F, L = log_parts + F;
+  int rem = L_last - F, L = log_parts + F;
   uint64_t nin = pl.nfront;
   int ks[8], ns = 0;
-  if (rem == 0) {
-    ks[ns++] = 0;
-  } else {
-    while (rem > 0) {
-      const int k = rem % 4 ? rem % 4 : 4;  // remainder first, then full 4-level stages
-      ks[ns++] = k;
-      rem -= k;
-    }
+  while (rem > 0) {
+    const int k = rem % 4 ? rem % 4 : 4;  // remainder first, then full 4-level stages
+    ks[ns++] = k;
+    rem -= k;
   }
+  ks[ns++] = k_last;
   uint64_t maxnodes = pl.nfront;
   for (int i = 0; i < ns; ++i) {
     Stage& st = pl.st[i];
     st.L_in = L;
     st.k = ks[i];
     st.nin = nin;
-    st.tile = (int)std::min<uint64_t>(nin, (uint64_t)(kExpOut >> st.k));
+    st.tile = (int)std::min<uint64_t>(nin, (uint64_t)(kExpOut >> std::min(st.k, 12)));
     st.final = i == ns - 1;
     L += st.k;
     nin <<= st.k;
@@ -610,6 +834,79 @@ TreePlan make_plan(int n, int log_parts, uint64_t prefix) {
   pl.max_nodes = maxnodes;
   return pl;
 }
+
+// ---- fused leaf stage + scan -----------------------------------------------------------------
+constexpr int kFusedTW = 8;       // tree waves per workgroup (the other 8 scan)
+constexpr int kFusedTileIn = 64;  // tree nodes entering a tile
+
+int fused_tile(int nq, uint32_t pitch, uint64_t nleaves, int num_cus) {
+  if (nq > 8) return 0;
+  const int vec = nq <= 2 ? 4 : 2;
+  const uint32_t cpr = pitch / (vec * 4);
+  if (cpr < (uint32_t)kColGroupLanes) return 0;  // records narrower than a wave row: 2-kernel path
+  const uint32_t gy = (cpr + kColGroupLanes - 1) / kColGroupLanes;
+  if (gy > 4) return 0;
+  // >= 4 tiles per CU so the tree runs under the scan; 4096-leaf tiles only for nrp <= 2
+  if (nq <= 2 && nleaves >= (uint64_t)4096 * num_cus * 4) return 4096;
+  if (nleaves >= (uint64_t)1024 * num_cus * 2) return 1024;
+  return 0;
+}
+
+template <int NQ, int TILE>
+static hipError_t fused_nq(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb,
+                           const uint8_t* shard, const ScanShape& sh, uint8_t* slabs, int buf,
+                           hipStream_t s) {
+  constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : 8));
+  constexpr int VEC = NQ <= 2 ? 4 : 2;
+  const Stage& st = pl.st[pl.nstages - 1];
+  const uint64_t ntiles = pl.nleaves / TILE;
+  hipLaunchKernelGGL((k_fused<NQ, NRP, VEC, true, kFusedTW, TILE, 4>), dim3(sh.grid.x),
+                     dim3(kFusedThreads), 0, s, d_key, nb.s[buf], nb.t[buf], st.L_in, st.k,
+                     ntiles, shard, sh.pitch, sh.cpr, sh.grid.y, slabs);
+  return hipGetLastError();
+}
+
+ScanShape make_fused_shape(uint64_t nleaves, uint32_t pitch, int nq, int num_cus, int tile) {
+  ScanShape sh{};
+  sh.nq = nq;
+  sh.nrp = nq == 1 ? 1 : (nq == 2 ? 2 : (nq <= 4 ? 4 : 8));
+  sh.vec = nq <= 2 ? 4 : 2;
+  sh.pitch = pitch;
+  sh.cpr = pitch / (sh.vec * 4);
+  sh.uniform = true;
+  const uint32_t gy = (sh.cpr + kColGroupLanes - 1) / kColGroupLanes;
+  const uint64_t ntiles = nleaves / tile;
+  sh.grid = dim3((unsigned)std::min<uint64_t>(ntiles, (uint64_t)num_cus), gy);
+  sh.slab_bytes = (uint32_t)(nq * kColGroupLanes * sh.vec * 4);
+  return sh;
+}
+
+hipError_t launch_fused(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb,
+                        const uint8_t* shard, const ScanShape& sh, uint8_t* slabs, int tile,
+                        hipStream_t s) {
+  const int buf = (pl.nstages - 1) & 1;  // node buffer holding the last stage's input
+  if (tile == 4096) {
+    switch (sh.nq) {
+      case 1: return fused_nq<1, 4096>(pl, d_key, nb, shard, sh, slabs, buf, s);
+      case 2: return fused_nq<2, 4096>(pl, d_key, nb, shard, sh, slabs, buf, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if (tile != 1024) return hipErrorInvalidValue;
+  switch (sh.nq) {
+    case 1: return fused_nq<1, 1024>(pl, d_key, nb, shard, sh, slabs, buf, s);
+    case 2: return fused_nq<2, 1024>(pl, d_key, nb, shard, sh, slabs, buf, s);
+    case 3: return fused_nq<3, 1024>(pl, d_key, nb, shard, sh, slabs, buf, s);
+    case 4: return fused_nq<4, 1024>(pl, d_key, nb, shard, sh, slabs, buf, s);
+    case 5: return fused_nq<5, 1024>(pl, d_key, nb, shard, sh, slabs, buf, s);
+    case 6: return fused_nq<6, 1024>(pl, d_key, nb, shard, sh, slabs, buf, s);
+    case 7: return fused_nq<7, 1024>(pl, d_key, nb, shard, sh, slabs, buf, s);
+    case 8: return fused_nq<8, 1024>(pl, d_key, nb, shard, sh, slabs, buf, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+int fused_k(int tile) { return tile == 4096 ? 6 : (tile == 1024 ? 4 : 0); }
 
 hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys, int p, int n,
                            int nq, int party0, DevKey* d_keys, hipStream_t s) {
