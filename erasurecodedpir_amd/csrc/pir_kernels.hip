@@ -504,7 +504,8 @@ struct FusedSmem {
   uint32_t tb[TILE / 4];
   uint8_t ring[2][TILE * NRP];
   uint32_t red[GYMAX][NQ * kColGroupLanes * VEC];
-  uint32_t bar, ready, consumed;
+  uint32_t bar, ready;
+  uint32_t consumed[2];  // per ring slot: scan-wave arrivals (a wave may run a tile ahead)
 };
 
 __device__ __forceinline__ uint32_t lds_load(const uint32_t* p) {
@@ -539,7 +540,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
   __shared__ Smem sm;
   load_tables(sm.tab);
   for (int i = threadIdx.x; i < GYMAX * NQ * GW; i += blockDim.x) (&sm.red[0][0])[i] = 0;
-  if (threadIdx.x == 0) { sm.bar = 0; sm.ready = 0; sm.consumed = 0; }
+  if (threadIdx.x == 0) { sm.bar = 0; sm.ready = 0; sm.consumed[0] = 0; sm.consumed[1] = 0; }
   __syncthreads();
 
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -568,7 +569,9 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
       const uint64_t tile = b + (uint64_t)i * G;
       const uint64_t ibase = tile * tile_in;
       uint8_t* ring = sm.ring[i & 1];
-      if (i >= 2) lds_wait_geq(&sm.consumed, (i - 1) * SW);  // slot free: tile i-2 scanned
+      // slot i&1 free: every scan wave finished tile i-2 (per-slot count: no wave can arrive
+      // twice on a slot before the tree refills it)
+      if (i >= 2) lds_wait_geq(&sm.consumed[i & 1], (i >> 1) * SW);
       int buf = (k - 1) & 1;
       {
         uint4* s0 = buf ? sm.sb : sm.sa;
@@ -681,7 +684,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
             }
         }
       }
-      lds_signal(&sm.consumed);
+      lds_signal(&sm.consumed[i & 1]);
     }
     if (active) {
       const uint32_t wbase = (UNI ? lane : chunk) * VEC;
