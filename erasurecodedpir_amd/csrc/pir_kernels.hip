@@ -94,11 +94,26 @@ struct Bits {
 // ------------------------------------------------------------------------------------------
 constexpr int kFrontThreads = 512;
 constexpr int kFrontCap = 256;  // nodes per LDS level buffer (e <= 9)
+constexpr int kFrontCwLevels = 24;  // levels whose CWs are staged in LDS (F <= 16 + parts)
 struct FrontSmem {
   uint32_t tab[2 * 256 * 32];
   uint32_t s[2][kFrontCap][4];
   uint32_t t[2][kFrontCap];
+  uint4 scw[kFrontCwLevels * kMaxCW];
+  uint32_t tcw[kFrontCwLevels * kMaxCW];
 };
+
+// level_cw from LDS-staged correction words (frontier: no scalar-cache misses per level)
+__device__ __forceinline__ void level_cw_lds(const uint4* scw, const uint32_t* tcw, int L,
+                                             uint32_t t, uint32_t pm1, uint4& cs, uint32_t& ct) {
+  cs = make_uint4(0, 0, 0, 0);
+  ct = 0;
+  for (uint32_t j = 0; j < pm1; ++j) {
+    const uint32_t m = 0u - ((t >> j) & 1u);
+    cs = xor4(cs, and4(scw[L * kMaxCW + j], m));
+    ct ^= tcw[L * kMaxCW + j] & m;
+  }
+}
 
 __device__ __forceinline__ uint32_t word_of(const uint4& v, uint32_t q) {
   return q == 0 ? v.x : (q == 1 ? v.y : (q == 2 ? v.z : v.w));
@@ -116,7 +131,18 @@ __global__ __launch_bounds__(kFrontThreads) void k_frontier(
   const uint32_t ptq = q == 3 ? (role << 24) : 0u;  // CTR block `role`: BE128(role)
   const int lane = threadIdx.x & 63;
   const int g16 = lane & ~15;
+  const int nlev = log_parts + g + e;  // levels this kernel expands
+  const bool cw_lds = nlev <= kFrontCwLevels;
+  if (cw_lds)
+    for (int i = threadIdx.x; i < nlev * kMaxCW; i += blockDim.x) {
+      sm.scw[i] = K->scw[i];
+      sm.tcw[i] = K->tcw[i];
+    }
   __syncthreads();
+  auto cw = [&](int L, uint32_t tv, uint4& cs, uint32_t& ct) {
+    if (cw_lds) level_cw_lds(sm.scw, sm.tcw, L, tv, B.pm1, cs, ct);
+    else level_cw(K, L, tv, B.pm1, cs, ct);
+  };
 
   // ---- descent (redundant in every 16-lane group) --------------------------------------
   const int D0 = log_parts + g;
@@ -126,7 +152,7 @@ __global__ __launch_bounds__(kFrontThreads) void k_frontier(
     const uint32_t o = aes_col(T, sq, ptq, mq1, mq2);
     uint4 cs;
     uint32_t ct;
-    level_cw(K, L, t, B.pm1, cs, ct);
+    cw(L, t, cs, ct);
     const uint32_t bit = (uint32_t)((path >> (D0 - 1 - L)) & 1u);
     const uint32_t oc = o ^ word_of(cs, q);
     sq = (uint32_t)__shfl((int)oc, g16 | (int)(bit << 2) | (int)q, 64);
@@ -155,7 +181,7 @@ __global__ __launch_bounds__(kFrontThreads) void k_frontier(
         const uint32_t o = aes_col(T, s_in, ptq, mq1, mq2);
         uint4 cs;
         uint32_t ct;
-        level_cw(K, L, t_in, B.pm1, cs, ct);
+        cw(L, t_in, cs, ct);
         if (role < 2) {
           const uint32_t v = o ^ word_of(cs, q);
           if (last) reinterpret_cast<uint32_t*>(out_s + obase + 2 * u + role)[q] = v;
@@ -650,6 +676,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
         for (int v = 0; v < VEC; ++v) Z[a][kk][v] = 0;
     const uint32_t ngroups = (TILE + rpw - 1) / rpw;
     constexpr int U = SW >= 8 ? 8 : 16;
+    // memory-bound waves go first: their few VALU ops gate the next loads
+    __builtin_amdgcn_s_setprio(2);
     for (uint32_t i = 0; i < my_tiles; ++i) {
       const uint64_t tile = b + (uint64_t)i * G;
       const uint8_t* ring = sm.ring[i & 1];
@@ -668,18 +696,34 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
             if (ok) x[u] = load_chunk<VEC>(base + (uint64_t)rl * pitch);
             else
               for (int v = 0; v < VEC; ++v) x[u].v[v] = 0;
-            cf[u] = ok ? load_coef<NRP>(ring, rl) : make_uint4(0, 0, 0, 0);
+            if (UNI) {  // one record per wave row: the coefficients are wave-uniform
+              const uint32_t gu = __builtin_amdgcn_readfirstlane(gi);
+              uint4 c4 = gu < ngroups ? load_coef<NRP>(ring, gu) : make_uint4(0, 0, 0, 0);
+              cf[u] = make_uint4(__builtin_amdgcn_readfirstlane(c4.x), __builtin_amdgcn_readfirstlane(c4.y),
+                                 __builtin_amdgcn_readfirstlane(c4.z), __builtin_amdgcn_readfirstlane(c4.w));
+            } else {
+              cf[u] = ok ? load_coef<NRP>(ring, rl) : make_uint4(0, 0, 0, 0);
+            }
           }
 #pragma unroll
           for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int a = 0; a < NQ; ++a) {
               const uint32_t ca = coef_byte(cf[u], a);
+              if (UNI) {  // scalar branches: ~4 XORs per dword instead of 8 masked ones
 #pragma unroll
-              for (int kk = 0; kk < 8; ++kk) {
-                const uint32_t m = 0u - ((ca >> kk) & 1u);
+                for (int kk = 0; kk < 8; ++kk)
+                  if (ca & (1u << kk)) {
 #pragma unroll
-                for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= x[u].v[v] & m;
+                    for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= x[u].v[v];
+                  }
+              } else {
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk) {
+                  const uint32_t m = 0u - ((ca >> kk) & 1u);
+#pragma unroll
+                  for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= x[u].v[v] & m;
+                }
               }
             }
         }
@@ -827,7 +871,10 @@ TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last) {
     st.L_in = L;
     st.k = ks[i];
     st.nin = nin;
-    st.tile = (int)std::min<uint64_t>(nin, (uint64_t)(kExpOut >> std::min(st.k, 12)));
+    // <= 4096 outputs per workgroup, but >= 256 workgroups when the level is wide enough
+    uint64_t tl = std::min<uint64_t>(nin, (uint64_t)(kExpOut >> std::min(st.k, 12)));
+    while (tl > 64 && nin / tl < 256) tl >>= 1;
+    st.tile = (int)tl;
     st.final = i == ns - 1;
     L += st.k;
     nin <<= st.k;
