@@ -150,8 +150,15 @@ int pick_chunks(const pir::TreePlan& pl, int num_cus) {
 // with the tree rooted at `prefix` (depth log_parts_total).  d_key points at ONE parsed key.
 //   s  : key prep, frontier, leaves(0..C-1), [join], reduce
 //   aux: scan(j) after leaves(j)  -- so leaves(j+1) overlaps scan(j)
-int answer_fused(pir_engine* e, const pir::DevKey* d_key, int log_parts_total, uint64_t prefix,
+pir::KeySrc key_src(pir_engine* e, const uint8_t* d_raw) {
+  const auto& c = e->cfg;
+  return pir::KeySrc{d_raw, c.num_parties, c.log_num_records, c.num_rounds, c.party_index - 1,
+                     e->d_keys};
+}
+
+int answer_fused(pir_engine* e, const uint8_t* d_raw, int log_parts_total, uint64_t prefix,
                  uint64_t row0, uint8_t* d_out, hipStream_t s, int tile) {
+  const pir::DevKey* d_key = e->d_keys;
   const auto& c = e->cfg;
   const pir::TreePlan pl =
       pir::make_plan(c.log_num_records, log_parts_total, prefix, pir::fused_k(tile));
@@ -163,7 +170,7 @@ int answer_fused(pir_engine* e, const pir::DevKey* d_key, int log_parts_total, u
   e->last_fused = 1;
   hipEvent_t* ev = e->ev;
   if (ev) HIP_TRY(hipEventRecord(ev[EV_KEY], s));
-  HIP_TRY(pir::launch_frontier(pl, d_key, e->nodes, s));
+  HIP_TRY(pir::launch_frontier(pl, key_src(e, d_raw), e->nodes, s));
   HIP_TRY(pir::launch_stages(pl, d_key, e->nodes, 0, 1, e->d_c, e->nrp, s, 0, pl.nstages - 1));
   if (ev) {
     HIP_TRY(hipEventRecord(ev[EV_FRONT], s));
@@ -182,12 +189,13 @@ int answer_fused(pir_engine* e, const pir::DevKey* d_key, int log_parts_total, u
   return PIR_OK;
 }
 
-int answer_core(pir_engine* e, const pir::DevKey* d_key, int log_parts_total, uint64_t prefix,
+int answer_core(pir_engine* e, const uint8_t* d_raw, int log_parts_total, uint64_t prefix,
                 uint64_t row0, uint8_t* d_out, hipStream_t s) {
   const auto& c = e->cfg;
+  const pir::DevKey* d_key = e->d_keys;
   const uint64_t nleaves = 1ull << (c.log_num_records - log_parts_total);
   const int tile = e->allow_fused ? pir::fused_tile(c.num_rounds, e->pitch, nleaves, e->num_cus) : 0;
-  if (tile) return answer_fused(e, d_key, log_parts_total, prefix, row0, d_out, s, tile);
+  if (tile) return answer_fused(e, d_raw, log_parts_total, prefix, row0, d_out, s, tile);
   e->last_fused = 0;
   const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix);
   const int C = pick_chunks(pl, e->num_cus);
@@ -198,7 +206,7 @@ int answer_core(pir_engine* e, const pir::DevKey* d_key, int log_parts_total, ui
   if (rc) return rc;
   hipEvent_t* ev = e->ev;
   if (ev) HIP_TRY(hipEventRecord(ev[EV_KEY], s));
-  HIP_TRY(pir::launch_frontier(pl, d_key, e->nodes, s));
+  HIP_TRY(pir::launch_frontier(pl, key_src(e, d_raw), e->nodes, s));
   HIP_TRY(pir::launch_stages(pl, d_key, e->nodes, 0, 1, e->d_c, e->nrp, s, 0, pl.nstages - 1));
   if (ev) HIP_TRY(hipEventRecord(ev[EV_FRONT], s));
   for (int j = 0; j < C; ++j) {
@@ -281,10 +289,9 @@ int answer_dev_locked(pir_engine* e, const uint8_t* d_key, uint8_t* d_result, hi
     e->ev = nullptr;
     return PIR_OK;
   }
-  HIP_TRY(pir::launch_key_prep(d_key, e->key_len, 1, c.num_parties, c.log_num_records,
-                               c.num_rounds, c.party_index - 1, e->d_keys, s));
   uint8_t* part_out = e->comm ? e->d_part : d_result;
-  int rc = answer_core(e, e->d_keys, c.log_num_partitions, (uint64_t)c.partition_index, 0,
+  // the key is parsed inside the frontier kernel (k_key_prep only when the tree is very deep)
+  int rc = answer_core(e, d_key, c.log_num_partitions, (uint64_t)c.partition_index, 0,
                        part_out, s);
   if (rc) return rc;
   if (e->comm) {
@@ -520,11 +527,9 @@ int pir_engine_answer_slice(pir_engine_t* e, const uint8_t* key, int thread_num,
   // set (both branches of server.cpp:526-541 are identical); mirrored here.
   memcpy(e->h_key, key, e->key_len);
   HIP_TRY(hipMemcpyAsync(e->d_key_raw, e->h_key, e->key_len, hipMemcpyHostToDevice, e->stream));
-  HIP_TRY(pir::launch_key_prep(e->d_key_raw, e->key_len, 1, c.num_parties, c.log_num_records,
-                               c.num_rounds, c.party_index - 1, e->d_keys, e->stream));
   const uint64_t prefix = ((uint64_t)c.partition_index << lt) | (uint64_t)thread_num;
   const uint64_t row0 = (uint64_t)thread_num * (e->rows >> lt);
-  int rc = answer_core(e, e->d_keys, c.log_num_partitions + lt, prefix, row0, e->d_result,
+  int rc = answer_core(e, e->d_key_raw, c.log_num_partitions + lt, prefix, row0, e->d_result,
                        e->stream);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(e->h_res, e->d_result, out_bytes, hipMemcpyDeviceToHost, e->stream));
@@ -541,11 +546,9 @@ int pir_engine_eval_all(pir_engine_t* e, const uint8_t* key, uint8_t* out) {
   HIP_TRY(hipSetDevice(c.device));
   memcpy(e->h_key, key, e->key_len);
   HIP_TRY(hipMemcpyAsync(e->d_key_raw, e->h_key, e->key_len, hipMemcpyHostToDevice, e->stream));
-  HIP_TRY(pir::launch_key_prep(e->d_key_raw, e->key_len, 1, c.num_parties, c.log_num_records,
-                               c.num_rounds, c.party_index - 1, e->d_keys, e->stream));
   const pir::TreePlan pl =
       pir::make_plan(c.log_num_records, c.log_num_partitions, (uint64_t)c.partition_index);
-  HIP_TRY(pir::launch_frontier(pl, e->d_keys, e->nodes, e->stream));
+  HIP_TRY(pir::launch_frontier(pl, key_src(e, e->d_key_raw), e->nodes, e->stream));
   HIP_TRY(pir::launch_stages(pl, e->d_keys, e->nodes, 0, 1, e->d_c, e->nrp, e->stream));
   std::vector<uint8_t> ct((size_t)e->rows * e->nrp);
   HIP_TRY(hipMemcpyAsync(ct.data(), e->d_c, ct.size(), hipMemcpyDeviceToHost, e->stream));
@@ -630,7 +633,8 @@ int pir_engine_profile_phases(pir_engine_t* e, const uint8_t* d_key, int iters, 
     HIP_TRY(pir::launch_key_prep(d_key, e->key_len, 1, c.num_parties, c.log_num_records,
                                  c.num_rounds, c.party_index - 1, e->d_keys, s));
   HIP_TRY(hipEventRecord(ev[1], s));
-  for (int i = 0; i < iters; ++i) HIP_TRY(pir::launch_frontier(pl, e->d_keys, e->nodes, s));
+  for (int i = 0; i < iters; ++i)
+    HIP_TRY(pir::launch_frontier(pl, key_src(e, nullptr), e->nodes, s));
   HIP_TRY(hipEventRecord(ev[2], s));
   for (int i = 0; i < iters; ++i)
     HIP_TRY(pir::launch_stages(pl, e->d_keys, e->nodes, 0, 1, e->d_c, e->nrp, s));

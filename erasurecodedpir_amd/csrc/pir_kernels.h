@@ -55,7 +55,14 @@ void upload_aes_table(hipStream_t s);  // Te0 (computed on the host) -> __consta
 
 hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys, int p, int n,
                            int nq, int party0, DevKey* d_keys, hipStream_t s);
-hipError_t launch_frontier(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb,
+// Where the frontier gets the key: raw bytes (parsed in-kernel; the DevKey for the later
+// kernels is written to `key` by workgroup 0), or raw == nullptr: `key` already parsed.
+struct KeySrc {
+  const uint8_t* raw;
+  int p, n, nq, party0;
+  DevKey* key;
+};
+hipError_t launch_frontier(const TreePlan& pl, const KeySrc& ks, const NodeBufs& nb,
                            hipStream_t s);
 // expand stages [i0, i1) (i1 < 0: to the last) for chunk j of C of every stage's input range
 hipError_t launch_stages(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb, int j, int C,

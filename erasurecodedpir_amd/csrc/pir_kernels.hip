@@ -24,31 +24,37 @@ void upload_aes_table(hipStream_t s) { upload_te0(s); }
 // ------------------------------------------------------------------------------------------
 // k_key_prep: raw key bytes -> DevKey (one workgroup per key)
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_key_prep(const uint8_t* __restrict__ raw,
-                                                  size_t key_stride, int p, int n, int nq,
-                                                  int party0, DevKey* __restrict__ out) {
-  const uint8_t* key = raw + blockIdx.x * key_stride;
-  DevKey* K = out + blockIdx.x;
+__device__ __forceinline__ uint32_t load_le32(const uint8_t* b) {
+  return b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+}
+__device__ __forceinline__ uint4 load_le128(const uint8_t* b) {
+  return make_uint4(load_le32(b), load_le32(b + 4), load_le32(b + 8), load_le32(b + 12));
+}
+
+// sCW[L][j] / tCW[L][j] of the raw key (dpf_tree.cpp:506-513): tCW bytes packed to bits
+__device__ __forceinline__ void parse_cw(const uint8_t* key, int p, int L, int j, uint4& scw,
+                                         uint32_t& tcw) {
+  const int pm1 = p - 1, CWk = 16 + 2 * p - 2, CW = pm1 * CWk;
+  const uint8_t* cw = key + 16 + L * CW + j * CWk;
+  scw = load_le128(cw);
+  uint32_t tb = 0;
+  for (int k = 0; k < 2 * pm1; ++k) tb |= (uint32_t)(cw[16 + k] & 1u) << k;
+  tcw = tb;
+}
+
+// the whole DevKey, parsed by the threads of one workgroup
+__device__ void parse_key(const uint8_t* __restrict__ key, int p, int n, int nq, int party0,
+                          DevKey* __restrict__ K) {
   const int pm1 = p - 1, CWk = 16 + 2 * p - 2, CW = pm1 * CWk;
   const int tid = threadIdx.x;
   if (tid == 0) {
-    uint32_t w[4];
-    for (int i = 0; i < 4; ++i)
-      w[i] = key[4 * i] | (key[4 * i + 1] << 8) | (key[4 * i + 2] << 16) | ((uint32_t)key[4 * i + 3] << 24);
-    K->root_seed = make_uint4(w[0], w[1], w[2], w[3]);
-    K->root_t = party0 >= 1 ? (1u << (party0 - 1)) : 0u;
+    K->root_seed = load_le128(key);
+    K->root_t = party0 >= 1 ? (1u << (party0 - 1)) : 0u;  // dpf_tree.cpp:496-502
     K->p = p; K->n = n; K->nq = nq;
   }
   for (int e = tid; e < n * pm1; e += blockDim.x) {
     const int L = e / pm1, j = e - L * pm1;
-    const uint8_t* cw = key + 16 + L * CW + j * CWk;  // dpf_tree.cpp:506-513
-    uint32_t w[4];
-    for (int i = 0; i < 4; ++i)
-      w[i] = cw[4 * i] | (cw[4 * i + 1] << 8) | (cw[4 * i + 2] << 16) | ((uint32_t)cw[4 * i + 3] << 24);
-    K->scw[L * kMaxCW + j] = make_uint4(w[0], w[1], w[2], w[3]);
-    uint32_t tb = 0;
-    for (int k = 0; k < 2 * pm1; ++k) tb |= (uint32_t)(cw[16 + k] & 1u) << k;
-    K->tcw[L * kMaxCW + j] = tb;
+    parse_cw(key, p, L, j, K->scw[L * kMaxCW + j], K->tcw[L * kMaxCW + j]);
   }
   for (int j = tid; j < kMaxCW; j += blockDim.x) {  // dpf_tree.cpp:515-519
     uint32_t w[4] = {0, 0, 0, 0};
@@ -57,6 +63,12 @@ __global__ __launch_bounds__(256) void k_key_prep(const uint8_t* __restrict__ ra
         w[a >> 2] |= (uint32_t)key[16 + n * CW + a * pm1 + j] << (8 * (a & 3));
     K->lastcw[j] = make_uint4(w[0], w[1], w[2], w[3]);
   }
+}
+
+__global__ __launch_bounds__(256) void k_key_prep(const uint8_t* __restrict__ raw,
+                                                  size_t key_stride, int p, int n, int nq,
+                                                  int party0, DevKey* __restrict__ out) {
+  parse_key(raw + blockIdx.x * key_stride, p, n, nq, party0, out + blockIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -94,7 +106,7 @@ struct Bits {
 // ------------------------------------------------------------------------------------------
 constexpr int kFrontThreads = 512;
 constexpr int kFrontCap = 256;  // nodes per LDS level buffer (e <= 9)
-constexpr int kFrontCwLevels = 24;  // levels whose CWs are staged in LDS (F <= 16 + parts)
+constexpr int kFrontCwLevels = 32;  // levels whose CWs are staged in LDS (F <= 16 + parts)
 struct FrontSmem {
   uint32_t tab[2 * 256 * 32];
   uint32_t s[2][kFrontCap][4];
@@ -120,12 +132,18 @@ __device__ __forceinline__ uint32_t word_of(const uint4& v, uint32_t q) {
 }
 
 __global__ __launch_bounds__(kFrontThreads) void k_frontier(
-    const DevKey* __restrict__ K, uint64_t prefix, int log_parts, int g, int e,
-    uint4* __restrict__ out_s, uint32_t* __restrict__ out_t) {
+    const uint8_t* __restrict__ raw, int p, int n, int nq, int party0, DevKey* __restrict__ K,
+    uint64_t prefix, int log_parts, int g, int e, uint4* __restrict__ out_s,
+    uint32_t* __restrict__ out_t) {
+  // raw != nullptr: parse the key here (every workgroup stages the CWs it needs in LDS;
+  // workgroup 0 also writes the full DevKey for the later kernels).  raw == nullptr: K was
+  // written by k_key_prep.
   __shared__ FrontSmem sm;
+  __shared__ uint4 root_seed;
+  __shared__ uint32_t root_t;
   load_tables(sm.tab);
   const Tab T{reinterpret_cast<const char*>(sm.tab), (threadIdx.x & 31u) * 4u};
-  const Bits B(K->p);
+  const Bits B((uint32_t)p);
   const uint32_t q = threadIdx.x & 3u, role = (threadIdx.x >> 2) & 3u;
   const uint32_t mq1 = q >= 1 ? 0xffffffffu : 0u, mq2 = q >= 2 ? 0xffffffffu : 0u;
   const uint32_t ptq = q == 3 ? (role << 24) : 0u;  // CTR block `role`: BE128(role)
@@ -133,40 +151,59 @@ __global__ __launch_bounds__(kFrontThreads) void k_frontier(
   const int g16 = lane & ~15;
   const int nlev = log_parts + g + e;  // levels this kernel expands
   const bool cw_lds = nlev <= kFrontCwLevels;
-  if (cw_lds)
-    for (int i = threadIdx.x; i < nlev * kMaxCW; i += blockDim.x) {
-      sm.scw[i] = K->scw[i];
-      sm.tcw[i] = K->tcw[i];
+  if (raw) {
+    if (blockIdx.x == 0) parse_key(raw, p, n, nq, party0, K);
+    for (int i = threadIdx.x; i < nlev * (p - 1); i += blockDim.x) {
+      const int L = i / (p - 1), j = i - L * (p - 1);
+      parse_cw(raw, p, L, j, sm.scw[L * kMaxCW + j], sm.tcw[L * kMaxCW + j]);
     }
+    if (threadIdx.x == 0) {
+      root_seed = load_le128(raw);
+      root_t = party0 >= 1 ? (1u << (party0 - 1)) : 0u;
+    }
+  } else {
+    if (cw_lds)
+      for (int i = threadIdx.x; i < nlev * kMaxCW; i += blockDim.x) {
+        sm.scw[i] = K->scw[i];
+        sm.tcw[i] = K->tcw[i];
+      }
+    if (threadIdx.x == 0) {
+      root_seed = K->root_seed;
+      root_t = K->root_t;
+    }
+  }
   __syncthreads();
   auto cw = [&](int L, uint32_t tv, uint4& cs, uint32_t& ct) {
     if (cw_lds) level_cw_lds(sm.scw, sm.tcw, L, tv, B.pm1, cs, ct);
     else level_cw(K, L, tv, B.pm1, cs, ct);
   };
 
-  // ---- descent (redundant in every 16-lane group) --------------------------------------
+  // ---- descent: wave 0 only (its 4 groups of 16 lanes compute the same node) -------------
   const int D0 = log_parts + g;
   const uint64_t path = (prefix << g) | blockIdx.x;
-  uint32_t sq = word_of(K->root_seed, q), t = K->root_t;
-  for (int L = 0; L < D0; ++L) {
-    const uint32_t o = aes_col(T, sq, ptq, mq1, mq2);
-    uint4 cs;
-    uint32_t ct;
-    cw(L, t, cs, ct);
-    const uint32_t bit = (uint32_t)((path >> (D0 - 1 - L)) & 1u);
-    const uint32_t oc = o ^ word_of(cs, q);
-    sq = (uint32_t)__shfl((int)oc, g16 | (int)(bit << 2) | (int)q, 64);
-    const uint32_t tb = ((uint32_t)__shfl((int)o, g16 | 8, 64) & B.tb_mask) ^ ct;
-    t = (tb >> (bit * B.pm1)) & B.tmask;
-  }
   const uint64_t obase = (uint64_t)blockIdx.x << e;
-  if (e == 0) {
-    if (threadIdx.x < 4) reinterpret_cast<uint32_t*>(out_s + blockIdx.x)[q] = sq;
-    if (threadIdx.x == 0) out_t[blockIdx.x] = t;
-    return;
+  if (threadIdx.x < 64) {
+    uint32_t sq = word_of(root_seed, q), t = root_t;
+    for (int L = 0; L < D0; ++L) {
+      const uint32_t o = aes_col(T, sq, ptq, mq1, mq2);
+      uint4 cs;
+      uint32_t ct;
+      cw(L, t, cs, ct);
+      const uint32_t bit = (uint32_t)((path >> (D0 - 1 - L)) & 1u);
+      const uint32_t oc = o ^ word_of(cs, q);
+      sq = (uint32_t)__shfl((int)oc, g16 | (int)(bit << 2) | (int)q, 64);
+      const uint32_t tb = ((uint32_t)__shfl((int)o, g16 | 8, 64) & B.tb_mask) ^ ct;
+      t = (tb >> (bit * B.pm1)) & B.tmask;
+    }
+    if (e == 0) {
+      if (threadIdx.x < 4) reinterpret_cast<uint32_t*>(out_s + blockIdx.x)[q] = sq;
+      if (threadIdx.x == 0) out_t[blockIdx.x] = t;
+    } else {
+      if (threadIdx.x < 4) sm.s[0][0][q] = sq;
+      if (threadIdx.x == 0) sm.t[0][0] = t;
+    }
   }
-  if (threadIdx.x < 4) sm.s[0][0][q] = sq;
-  if (threadIdx.x == 0) sm.t[0][0] = t;
+  if (e == 0) return;
   __syncthreads();
 
   // ---- breadth-first expansion, 32 nodes per pass ----------------------------------------
@@ -965,10 +1002,18 @@ hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys
   return hipGetLastError();
 }
 
-hipError_t launch_frontier(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb,
+hipError_t launch_frontier(const TreePlan& pl, const KeySrc& ks, const NodeBufs& nb,
                            hipStream_t s) {
-  hipLaunchKernelGGL(k_frontier, dim3(1u << pl.g), dim3(kFrontThreads), 0, s, d_key, pl.prefix,
-                     pl.log_parts, pl.g, pl.e, nb.s[0], nb.t[0]);
+  const int nlev = pl.log_parts + pl.g + pl.e;
+  const uint8_t* raw = ks.raw;
+  if (raw && nlev > kFrontCwLevels) {  // CWs read from global: parse in a kernel of its own
+    hipError_t err = launch_key_prep(raw, 0, 1, ks.p, ks.n, ks.nq, ks.party0, ks.key, s);
+    if (err != hipSuccess) return err;
+    raw = nullptr;
+  }
+  hipLaunchKernelGGL(k_frontier, dim3(1u << pl.g), dim3(kFrontThreads), 0, s, raw, ks.p, ks.n,
+                     ks.nq, ks.party0, ks.key, pl.prefix, pl.log_parts, pl.g, pl.e, nb.s[0],
+                     nb.t[0]);
   return hipGetLastError();
 }
 
