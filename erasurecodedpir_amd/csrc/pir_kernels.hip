@@ -930,9 +930,8 @@ int fused_tile(int nq, uint32_t pitch, uint64_t nleaves, int num_cus) {
   if (nq > 8) return 0;
   const int vec = nq <= 2 ? 4 : 2;
   const uint32_t cpr = pitch / (vec * 4);
-  if (cpr < (uint32_t)kColGroupLanes) return 0;  // records narrower than a wave row: 2-kernel path
   const uint32_t gy = (cpr + kColGroupLanes - 1) / kColGroupLanes;
-  if (gy > 4) return 0;
+  if (gy > 4) return 0;  // > 4 column groups: more than the scan waves can split
   // >= 4 tiles per CU so the tree runs under the scan; 4096-leaf tiles only for nrp <= 2
   if (nq <= 2 && nleaves >= (uint64_t)4096 * num_cus * 4) return 4096;
   if (nleaves >= (uint64_t)1024 * num_cus * 2) return 1024;
@@ -947,9 +946,14 @@ static hipError_t fused_nq(const TreePlan& pl, const DevKey* d_key, const NodeBu
   constexpr int VEC = NQ <= 2 ? 4 : 2;
   const Stage& st = pl.st[pl.nstages - 1];
   const uint64_t ntiles = pl.nleaves / TILE;
-  hipLaunchKernelGGL((k_fused<NQ, NRP, VEC, true, kFusedTW, TILE, 4>), dim3(sh.grid.x),
-                     dim3(kFusedThreads), 0, s, d_key, nb.s[buf], nb.t[buf], st.L_in, st.k,
-                     ntiles, shard, sh.pitch, sh.cpr, sh.grid.y, slabs);
+  if (sh.uniform)
+    hipLaunchKernelGGL((k_fused<NQ, NRP, VEC, true, kFusedTW, TILE, 4>), dim3(sh.grid.x),
+                       dim3(kFusedThreads), 0, s, d_key, nb.s[buf], nb.t[buf], st.L_in, st.k,
+                       ntiles, shard, sh.pitch, sh.cpr, sh.grid.y, slabs);
+  else  // several records per wave row: per-lane coefficients
+    hipLaunchKernelGGL((k_fused<NQ, NRP, VEC, false, kFusedTW, TILE, 1>), dim3(sh.grid.x),
+                       dim3(kFusedThreads), 0, s, d_key, nb.s[buf], nb.t[buf], st.L_in, st.k,
+                       ntiles, shard, sh.pitch, sh.cpr, 1u, slabs);
   return hipGetLastError();
 }
 
@@ -960,8 +964,8 @@ ScanShape make_fused_shape(uint64_t nleaves, uint32_t pitch, int nq, int num_cus
   sh.vec = nq <= 2 ? 4 : 2;
   sh.pitch = pitch;
   sh.cpr = pitch / (sh.vec * 4);
-  sh.uniform = true;
-  const uint32_t gy = (sh.cpr + kColGroupLanes - 1) / kColGroupLanes;
+  sh.uniform = sh.cpr >= (uint32_t)kColGroupLanes;
+  const uint32_t gy = sh.uniform ? (sh.cpr + kColGroupLanes - 1) / kColGroupLanes : 1;
   const uint64_t ntiles = nleaves / tile;
   sh.grid = dim3((unsigned)std::min<uint64_t>(ntiles, (uint64_t)num_cus), gy);
   sh.slab_bytes = (uint32_t)(nq * kColGroupLanes * sh.vec * 4);
