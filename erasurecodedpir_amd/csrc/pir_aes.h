@@ -4,8 +4,9 @@
 //
 // T-box form with TWO LDS tables, Te0[x] = {2S,S,S,3S} and Te2 = rotl16(Te0) = {S,3S,2S,S}
 // (S = the FIPS-197 S-box, computed on the host from the field definition), each replicated
-// 32x as [entry][lane & 31]: every lane of a 32-lane ds_read_b32 group reads its own bank,
-// conflict-free for any index pattern.  With Te1 = rotl8(Te0) and Te3 = rotl8(Te2) a column is
+// 32x per entry (row e = 32 copies of Te0[e], then 32 of Te2[e]): every lane of a 32-lane
+// ds_read_b32 group reads its own bank, conflict-free for any index pattern, and a lookup
+// address costs one v_perm_b32.  With Te1 = rotl8(Te0) and Te3 = rotl8(Te2) a column is
 //     Te0[a] ^ Te2[c] ^ rotl8(Te0[b] ^ Te2[d] ^ rotr8(k))
 // -- one v_alignbit and two v_bitop3 (3-input XOR) per column.  The last round and the key
 // schedule read S from byte 1/2 of Te0 and byte 0/3 of Te2.
@@ -33,37 +34,43 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 __device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
 __device__ __forceinline__ uint32_t rotr8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 8); }
 
-// byte k of w -> byte offset of its table row (entry stride 128 B)
-__device__ __forceinline__ uint32_t off0(uint32_t w) { return (w << 7) & 0x7f80u; }
-__device__ __forceinline__ uint32_t off1(uint32_t w) { return (w >> 1) & 0x7f80u; }
-__device__ __forceinline__ uint32_t off2(uint32_t w) { return (w >> 9) & 0x7f80u; }
-__device__ __forceinline__ uint32_t off3(uint32_t w) { return (w >> 17) & 0x7f80u; }
+// LDS layout: 256 rows of 256 B, row e = [Te0[e] x 32 lanes | Te2[e] x 32 lanes].  The byte
+// address of a lookup is (index << 8) | (table << 7) | (lane & 31) << 2: index byte k of w lands in
+// address byte 1 and the per-lane constant in byte 0, so ONE v_perm_b32 forms the address.
+template <int K>
+__device__ __forceinline__ uint32_t tab_addr(uint32_t w, uint32_t lane_part) {
+  // bytes of {w, lane_part}: 0-3 = lane_part, 4-7 = w; 0x0c = zero
+  return __builtin_amdgcn_perm(w, lane_part, 0x0c0c0000u | ((4u + K) << 8));
+}
 
 struct Tab {
-  const char* base;  // LDS: Te0 replicated, then Te2 replicated
-  uint32_t lane4;    // (lane & 31) * 4
-  __device__ __forceinline__ uint32_t t0(uint32_t off) const {
-    return *reinterpret_cast<const uint32_t*>(base + (off | lane4));
+  const char* base;  // LDS: the interleaved table (64 KiB)
+  uint32_t l0, l2;   // (lane & 31) * 4, and the same + 128 (the Te2 half of a row)
+  __device__ __forceinline__ explicit Tab(const void* lds)
+      : base(reinterpret_cast<const char*>(lds)), l0((threadIdx.x & 31u) * 4u), l2(l0 | 128u) {}
+  template <int K>
+  __device__ __forceinline__ uint32_t t0(uint32_t w) const {  // Te0[byte K of w]
+    return *reinterpret_cast<const uint32_t*>(base + tab_addr<K>(w, l0));
   }
-  __device__ __forceinline__ uint32_t t2(uint32_t off) const {
-    return *reinterpret_cast<const uint32_t*>(base + kTeBytes + (off | lane4));
+  template <int K>
+  __device__ __forceinline__ uint32_t t2(uint32_t w) const {  // Te2[byte K of w]
+    return *reinterpret_cast<const uint32_t*>(base + tab_addr<K>(w, l2));
   }
 };
 
-// fill both replicated tables (all threads of the block)
+// fill the interleaved table (all threads of the block)
 __device__ __forceinline__ void load_tables(uint32_t* lds) {
-  for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) {
-    const uint32_t v = c_te0[i >> 5];
-    lds[i] = v;
-    lds[256 * 32 + i] = __builtin_amdgcn_alignbit(v, v, 16);
+  for (int i = threadIdx.x; i < 256 * 64; i += blockDim.x) {
+    const uint32_t v = c_te0[i >> 6];
+    lds[i] = (i & 32) ? __builtin_amdgcn_alignbit(v, v, 16) : v;
   }
 }
 
 // SubWord(RotWord(k3)) ^ rcon, then the word chain (FIPS-197 5.2)
 __device__ __forceinline__ void key_next(const Tab& T, uint32_t& k0, uint32_t& k1, uint32_t& k2,
                                          uint32_t& k3, uint32_t rcon) {
-  const uint32_t t = (T.t2(off1(k3)) & 0xffu) | (T.t0(off2(k3)) & 0xff00u) |
-                     (T.t0(off3(k3)) & 0xff0000u) | (T.t2(off0(k3)) & 0xff000000u);
+  const uint32_t t = (T.t2<1>(k3) & 0xffu) | (T.t0<2>(k3) & 0xff00u) |
+                     (T.t0<3>(k3) & 0xff0000u) | (T.t2<0>(k3) & 0xff000000u);
   k0 = xor3(k0, t, rcon);
   k1 ^= k0;
   k2 ^= k1;
@@ -74,18 +81,18 @@ __device__ __forceinline__ void key_next(const Tab& T, uint32_t& k0, uint32_t& k
 __device__ __forceinline__ void round_row(const Tab& T, uint32_t& w0, uint32_t& w1, uint32_t& w2,
                                           uint32_t& w3, uint32_t kr0, uint32_t kr1, uint32_t kr2,
                                           uint32_t kr3) {
-  const uint32_t n0 = xor3(T.t0(off0(w0)), T.t2(off2(w2)), rotl8(xor3(T.t0(off1(w1)), T.t2(off3(w3)), kr0)));
-  const uint32_t n1 = xor3(T.t0(off0(w1)), T.t2(off2(w3)), rotl8(xor3(T.t0(off1(w2)), T.t2(off3(w0)), kr1)));
-  const uint32_t n2 = xor3(T.t0(off0(w2)), T.t2(off2(w0)), rotl8(xor3(T.t0(off1(w3)), T.t2(off3(w1)), kr2)));
-  const uint32_t n3 = xor3(T.t0(off0(w3)), T.t2(off2(w1)), rotl8(xor3(T.t0(off1(w0)), T.t2(off3(w2)), kr3)));
+  const uint32_t n0 = xor3(T.t0<0>(w0), T.t2<2>(w2), rotl8(xor3(T.t0<1>(w1), T.t2<3>(w3), kr0)));
+  const uint32_t n1 = xor3(T.t0<0>(w1), T.t2<2>(w3), rotl8(xor3(T.t0<1>(w2), T.t2<3>(w0), kr1)));
+  const uint32_t n2 = xor3(T.t0<0>(w2), T.t2<2>(w0), rotl8(xor3(T.t0<1>(w3), T.t2<3>(w1), kr2)));
+  const uint32_t n3 = xor3(T.t0<0>(w3), T.t2<2>(w1), rotl8(xor3(T.t0<1>(w0), T.t2<3>(w2), kr3)));
   w0 = n0; w1 = n1; w2 = n2; w3 = n3;
 }
 
 // last-round column from (w_c, w_c+1, w_c+2, w_c+3): SubBytes + ShiftRows + AddRoundKey
 __device__ __forceinline__ uint32_t last_col(const Tab& T, uint32_t a, uint32_t b, uint32_t c,
                                              uint32_t d, uint32_t k) {
-  uint32_t x = (T.t2(off0(a)) & 0xffu) | (T.t0(off1(b)) & 0xff00u);
-  x |= (T.t0(off2(c)) & 0xff0000u) | (T.t2(off3(d)) & 0xff000000u);
+  uint32_t x = (T.t2<0>(a) & 0xffu) | (T.t0<1>(b) & 0xff00u);
+  x |= (T.t0<2>(c) & 0xff0000u) | (T.t2<3>(d) & 0xff000000u);
   return x ^ k;
 }
 
@@ -156,14 +163,14 @@ __device__ __forceinline__ uint32_t aes_col(const Tab& T, uint32_t kq, uint32_t 
   for (int r = 0; r < 10; ++r) {
     // key schedule: k'_q = SubWordRot(k3) ^ rcon ^ (k_0 ^ ... ^ k_q)
     const uint32_t k3 = qperm<kQ3333>(kq);
-    const uint32_t t = (T.t2(off1(k3)) & 0xffu) | (T.t0(off2(k3)) & 0xff00u) |
-                       (T.t0(off3(k3)) & 0xff0000u) | (T.t2(off0(k3)) & 0xff000000u);
+    const uint32_t t = (T.t2<1>(k3) & 0xffu) | (T.t0<2>(k3) & 0xff00u) |
+                       (T.t0<3>(k3) & 0xff0000u) | (T.t2<0>(k3) & 0xff000000u);
     uint32_t pre = kq ^ (qperm<kQ0012>(kq) & mq1);
     pre ^= qperm<kQ0101>(pre) & mq2;
     kq = xor3(pre, t, kRcon[r]);
     const uint32_t b = qperm<kQ1230>(w), c = qperm<kQ2301>(w), d = qperm<kQ3012>(w);
     if (r < 9)
-      w = xor3(T.t0(off0(w)), T.t2(off2(c)), rotl8(xor3(T.t0(off1(b)), T.t2(off3(d)), rotr8(kq))));
+      w = xor3(T.t0<0>(w), T.t2<2>(c), rotl8(xor3(T.t0<1>(b), T.t2<3>(d), rotr8(kq))));
     else
       w = last_col(T, w, b, c, d, kq);
   }

@@ -41,7 +41,7 @@ __global__ __launch_bounds__(64) void k_keygen(int n, uint64_t index, const uint
                                                uint8_t* __restrict__ keys, int kl) {
   __shared__ KeygenSmem sm;
   load_tables(sm.tab);
-  const Tab T{reinterpret_cast<const char*>(sm.tab), (threadIdx.x & 31u) * 4u};
+  const Tab T(sm.tab);
   const int tid = threadIdx.x, pm1 = p - 1, CWk = 16 + 2 * p - 2, CW = pm1 * CWk;
   const uint32_t tbits = 2 * pm1;
   const uint32_t tb_mask = tbits >= 32 ? 0xffffffffu : ((1u << tbits) - 1u);

@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kFrontThreads) void k_frontier(
   __shared__ uint4 root_seed;
   __shared__ uint32_t root_t;
   load_tables(sm.tab);
-  const Tab T{reinterpret_cast<const char*>(sm.tab), (threadIdx.x & 31u) * 4u};
+  const Tab T(sm.tab);
   const Bits B((uint32_t)p);
   const uint32_t q = threadIdx.x & 3u, role = (threadIdx.x >> 2) & 3u;
   const uint32_t mq1 = q >= 1 ? 0xffffffffu : 0u, mq2 = q >= 2 ? 0xffffffffu : 0u;
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(kExpThreads) void k_expand(
   constexpr int NW = NRP <= 4 ? 1 : NRP / 4;
   __shared__ ExpSmem sm;
   load_tables(sm.tab);
-  const Tab T{reinterpret_cast<const char*>(sm.tab), (threadIdx.x & 31u) * 4u};
+  const Tab T(sm.tab);
   const Bits B(K->p);
   const uint64_t ibase = (uint64_t)blockIdx.x * tile;
   const uint64_t obase = ibase << k;
@@ -614,7 +614,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
 
   if (wave < (uint32_t)TW) {
     // ===================================== tree role ======================================
-    const Tab T{reinterpret_cast<const char*>(sm.tab), (threadIdx.x & 31u) * 4u};
+    const Tab T(sm.tab);
     const Bits B(K->p);
     const int tt = threadIdx.x, nt = TW * 64;
     uint32_t gen = 0;

@@ -16,6 +16,7 @@ python -c "import erasurecodedpir_amd as p; p.load()" || { echo "library does no
 [ -n "$SKIP_TESTS" ] || step pytest_gpu 900 python -m pytest tests -m gpu -x -q
 step bench_c2 300 python bench.py --steps 50 --warmup 5
 [ -n "$SKIP_C24" ] || step bench_c24 300 python bench.py --config c24 --steps 20 --warmup 3 --no-cpu
+for c in $EXTRA_CONFIGS; do step bench_$c 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu; done
 if [ -z "$SKIP_PROF" ]; then
   rm -rf gpurun_out/prof_c2
   step rocprof_c2 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2 -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu
