@@ -43,6 +43,10 @@ CONFIGS = {
     "c3": (24, 256, 2, 1, "configs[2] shape per query: one shard 2^24 x 256 B (queries answered one at a time)"),
     "c5": (24, 1024, 8, 5, "configs[4] per-GPU server: 2^24 x 1 KiB shard, p=8 (k=5, r=2), NUM_ROUNDS=5"),
 }
+# batched configs: a step answers `batch` keys (distinct indices) against the shard
+BATCH_CONFIGS = {
+    "c3b": (24, 256, 2, 1, 128, "configs[2]: 1 MI355X, one shard 2^24 x 256 B, 128 batched queries"),
+}
 
 
 def dist_env():
@@ -107,7 +111,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + sorted(BATCH_CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
@@ -127,6 +131,8 @@ def main():
     import erasurecodedpir_amd as pir
     from erasurecodedpir_amd.dist import broadcast_bytes, log2_exact
 
+    if args.config in BATCH_CONFIGS:
+        return run_batch(args, world, rank, local)
     n_local, efs, p, nq, workload = CONFIGS[args.config]
     g = log2_exact(world)
     n = n_local + g  # logical tree depth (weak scaling: 2^n_local records per GPU)
@@ -252,6 +258,98 @@ def main():
                                            args.cpu_budget)
         out["parity"]["gpu_equals_cpu_reference"] = out["cpu_baseline"]["bit_exact_vs_gpu"]
         del shard_rows
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_batch(args, world, rank, local):
+    """A step = `batch` keys answered against the device-resident shard (answer_batch_dev: one
+    shard pass per group of keys, one DPF tree per key).  value = effective GiB/s = keys x
+    logical shard bytes / time (every key's answer covers the whole shard)."""
+    import torch
+    import torch.distributed as dist
+    import erasurecodedpir_amd as pir
+    from erasurecodedpir_amd.dist import broadcast_bytes, log2_exact
+
+    n_local, efs, p, nq, nk, workload = BATCH_CONFIGS[args.config]
+    g = log2_exact(world)
+    n = n_local + g
+    eng = pir.Engine(p, 1, n, efs, nq, device=local, log_num_partitions=g, partition_index=rank)
+    eng.fill_shard_random(0xC0FFEE)
+    if world > 1:
+        uid = broadcast_bytes(pir.comm_unique_id() if rank == 0 else None)
+        eng.attach_comm(uid, world, rank)
+    rng = np.random.default_rng(int.from_bytes(
+        broadcast_bytes(os.urandom(8) if rank == 0 else None) if world > 1 else os.urandom(8), "little"))
+    idxs = [int(i) for i in rng.choice(1 << n, nk, replace=False)]
+    fcw = pir.final_cw(p, nq, 1)
+    keys = [pir.gen_keys(n, i, p, nq, fcw=fcw, seeds=rng.integers(0, 256, 16 * p, dtype=np.uint8).tobytes(),
+                         device=local) for i in idxs]
+    d_keys = eng.alloc_dev(eng.key_len * nk)
+    d_res = eng.alloc_dev(eng.answer_bytes * nk)
+    eng.h2d(d_keys, b"".join(k[0] for k in keys))
+
+    def barrier_sync():
+        eng.sync()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        eng.answer_batch_dev(d_keys, nk, d_res)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.answer_batch_dev(d_keys, nk, d_res)
+    barrier_sync()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms = dt / args.steps * 1e3
+    # one key alone (fused single-query path) and its tree / scan phases, for reference
+    alone = eng.profile_phases(d_keys, 5)
+    got = eng.d2h(d_res, eng.answer_bytes * nk).reshape(nk, nq, efs)
+    # correctness at full size: party-1 batch ^ party-2 batch == finalCW * record, every key
+    eng2 = pir.Engine(p, 2, n, efs, nq, device=local, log_num_partitions=g, partition_index=rank)
+    eng2.fill_shard_random(0xC0FFEE)
+    if world > 1:
+        uid2 = broadcast_bytes(pir.comm_unique_id() if rank == 0 else None)
+        eng2.attach_comm(uid2, world, rank)
+    got2 = eng2.answer_batch([k[1] for k in keys])
+    eng2.close()
+    tab = _gf_table(int(fcw[0]))
+    ok = True
+    for q, i in enumerate(idxs):
+        owner = i >> (n - g) if g else 0
+        rec = eng.shard_row(i - owner * eng.num_rows) if rank == owner else None
+        if world > 1:
+            rec = broadcast_from(rec, owner, efs)
+        ok &= bool(np.array_equal(got[q][0] ^ got2[q][0], tab[rec]))
+    shard_bytes = float(1 << n) * efs
+    out = {
+        "metric": METRIC,
+        "value": round(nk * shard_bytes / GIB / (ms / 1e3), 3),
+        "unit": "GiB/s",
+        "value_kind": "effective: keys x logical shard bytes / batch time",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": workload, "records": 1 << n, "record_bytes": efs, "parties": p,
+                   "num_rounds": nq, "batch": nk, "keys_per_shard_pass": eng.batch_group,
+                   "records_per_gpu": int(eng.num_rows), "dpf_depth": n,
+                   "parallelism": "split-shard" if world > 1 else "single"},
+        "ms_per_key": round(ms / nk, 5),
+        "keys_per_s": round(nk / (ms / 1e3), 1),
+        "shard_passes_per_step": -(-nk // eng.batch_group),
+        "single_key_phases_alone_ms": {k: round(v, 5) for k, v in alone.items()},
+        "parity": {"pir_record_recovered_all_keys": ok},
+    }
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

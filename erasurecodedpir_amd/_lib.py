@@ -75,6 +75,9 @@ PROTOTYPES = {
     "pir_engine_eval_all": (_I, [_P, _P, _P]),
     "pir_engine_answer_dev": (_I, [_P, _P, _P, _P]),
     "pir_engine_answer_batch_dev": (_I, [_P, _P, _I, _P, _P]),
+    "pir_engine_answer_batch": (_I, [_P, _P, _I, _P]),
+    "pir_engine_set_batch_group": (_I, [_P, _I]),
+    "pir_engine_batch_group": (_I, [_P]),
     "pir_engine_stream": (_P, [_P]),
     "pir_engine_sync": (_I, [_P]),
     "pir_engine_alloc_dev": (_I, [_P, _SZ, ctypes.POINTER(_P)]),

@@ -84,6 +84,7 @@ struct pir_engine {
   hipStream_t aux = nullptr;              // scan stream of the leaves/scan pipeline
   hipEvent_t ev_leaf[kMaxChunks] = {};    // leaves of chunk j written
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_cb_ready[2] = {}, ev_cb_free[2] = {};  // batched answers: share buffers
   int last_chunks = 1;
   int last_fused = 0;
   bool allow_fused = true;  // $PIR_FUSED=0 forces the 2-kernel path (A/B diagnostics)
@@ -97,6 +98,17 @@ struct pir_engine {
   size_t slab_cap = 0;
   uint8_t* d_part = nullptr;    // nq*efs partition answer
   uint8_t* d_gather = nullptr;  // nranks*nq*efs
+  // batched answers: interleaved shares of a key group, group answer, batch partition answer
+  uint8_t* d_cb = nullptr;
+  size_t cb_cap = 0;
+  pir::NodeBufs bnodes{};       // node buffers of a key group (G x max_nodes)
+  uint64_t bnodes_cap = 0;
+  uint8_t* d_gtmp = nullptr;    // 16*efs
+  uint8_t* d_bpart = nullptr;   // batch partition answers (split shard)
+  uint8_t* d_bgather = nullptr; // nranks x batch answers
+  size_t bpart_cap = 0, bgather_cap = 0;
+  int batch_group = 0;          // keys per shard pass (0: automatic; $PIR_BATCH_G)
+  int last_batch_group = 0;
   uint8_t* d_result = nullptr;  // nq*efs (host-API staging)
   uint8_t* h_key = nullptr;     // pinned
   uint8_t* h_res = nullptr;     // pinned
@@ -126,6 +138,16 @@ int ensure_batch(pir_engine* e, int nk) {
   HIP_TRY(hipMalloc(&e->d_key_raw, (size_t)nk * e->key_len));
   HIP_TRY(hipMalloc(&e->d_keys, (size_t)nk * sizeof(pir::DevKey)));
   e->max_batch = nk;
+  return PIR_OK;
+}
+
+int ensure_buf(uint8_t** p, size_t* cap, size_t bytes) {
+  if (bytes <= *cap) return PIR_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  HIP_TRY(hipMalloc(p, bytes));
+  *cap = bytes;
   return PIR_OK;
 }
 
@@ -228,6 +250,86 @@ int answer_core(pir_engine* e, const uint8_t* d_raw, int log_parts_total, uint64
   return PIR_OK;
 }
 
+// keys answered per shard pass: G keys x nrp share bytes per record (a power of two <= 16)
+int batch_group(const pir_engine* e) {
+  const int maxg = 16 / e->nrp;
+  int g = e->batch_group > 0 ? e->batch_group : 8 / std::min(e->nrp, 8);
+  g = std::max(1, std::min(g, maxg));
+  while (g & (g - 1)) g &= g - 1;  // power of two
+  return g;
+}
+
+// nk keys (raw, key_len apart) against one partition slice, one shard pass per group of G
+// keys: each key's tree (frontier + stages) writes its shares into slot g of the interleaved
+// coefficient rows cb[i][G*nrp]; one multi-round scan of G*nrp rounds answers the group
+// (round g*nrp + a = key g, round a).  d_out: nk x nq x efs.
+//   s  : trees of group j into share buffer j%2   (waits until scan j-2 has read it)
+//   aux: scan + reduce of group j                  (after the trees of group j)
+// so the trees of group j+1 run beside the scan of group j.
+int answer_batch_core(pir_engine* e, const uint8_t* d_raw, int nk, int log_parts_total,
+                      uint64_t prefix, uint64_t row0, uint8_t* d_out, hipStream_t s) {
+  const auto& c = e->cfg;
+  const int G = batch_group(e);
+  const int W = G * e->nrp;
+  e->last_batch_group = G;
+  e->last_fused = 0;
+  e->last_chunks = 1;
+  const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix);
+  const pir::ScanShape sh = pir::make_scan_shape(pl.nleaves, e->pitch, W, e->num_cus);
+  const size_t cb_bytes = (size_t)pl.nleaves * W;
+  int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
+  if (!rc) rc = ensure_buf(&e->d_cb, &e->cb_cap, 2 * cb_bytes);
+  if (!rc) rc = ensure_batch(e, nk);
+  if (rc) return rc;
+  if (!e->d_gtmp) HIP_TRY(hipMalloc(&e->d_gtmp, (size_t)16 * c.record_bytes));
+  const uint64_t need_nodes = (uint64_t)G * pl.max_nodes;
+  if (need_nodes > e->bnodes_cap) {
+    for (int i = 0; i < 2; ++i) {
+      if (e->bnodes.s[i]) (void)hipFree(e->bnodes.s[i]);
+      if (e->bnodes.t[i]) (void)hipFree(e->bnodes.t[i]);
+      e->bnodes.s[i] = nullptr;
+      e->bnodes.t[i] = nullptr;
+    }
+    e->bnodes_cap = 0;
+    for (int i = 0; i < 2; ++i) {
+      HIP_TRY(hipMalloc(&e->bnodes.s[i], need_nodes * sizeof(uint4)));
+      HIP_TRY(hipMalloc(&e->bnodes.t[i], need_nodes * sizeof(uint32_t)));
+    }
+    e->bnodes_cap = need_nodes;
+  }
+  const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
+  HIP_TRY(hipEventRecord(e->ev_fork, s));
+  HIP_TRY(hipStreamWaitEvent(e->aux, e->ev_fork, 0));
+  for (int q0 = 0, j = 0; q0 < nk; q0 += G, ++j) {
+    const int ng = std::min(G, nk - q0), b = j & 1;
+    uint8_t* cb = e->d_cb + b * cb_bytes;
+    if (j >= 2) HIP_TRY(hipStreamWaitEvent(s, e->ev_cb_free[b], 0));
+    // the ng trees of the group side by side: grid row y = key q0 + y
+    const pir::KeySrc ks{d_raw + (size_t)q0 * e->key_len, c.num_parties, c.log_num_records,
+                         c.num_rounds, c.party_index - 1, e->d_keys + q0};
+    HIP_TRY(pir::launch_frontier(pl, ks, e->bnodes, s, ng, (size_t)e->key_len, pl.max_nodes));
+    HIP_TRY(pir::launch_stages(pl, e->d_keys + q0, e->bnodes, 0, 1, cb, e->nrp, s, 0, -1, W, ng,
+                               pl.max_nodes, (uint32_t)e->nrp));
+    HIP_TRY(hipEventRecord(e->ev_cb_ready[b], s));
+    HIP_TRY(hipStreamWaitEvent(e->aux, e->ev_cb_ready[b], 0));
+    // slots g >= ng hold stale shares: their rounds are computed and dropped
+    HIP_TRY(pir::launch_scan(sh, e->d_shard + row0 * e->pitch, pl.nleaves, cb, e->d_slabs, false,
+                             e->aux));
+    HIP_TRY(hipEventRecord(e->ev_cb_free[b], e->aux));
+    uint8_t* dst = d_out + (size_t)q0 * out_bytes;
+    if (e->nrp == c.num_rounds && ng == G) {
+      HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, dst, e->aux));
+    } else {
+      HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, e->d_gtmp, e->aux));
+      HIP_TRY(hipMemcpy2DAsync(dst, out_bytes, e->d_gtmp, (size_t)e->nrp * c.record_bytes,
+                               out_bytes, ng, hipMemcpyDeviceToDevice, e->aux));
+    }
+  }
+  HIP_TRY(hipEventRecord(e->ev_join, e->aux));
+  HIP_TRY(hipStreamWaitEvent(s, e->ev_join, 0));
+  return PIR_OK;
+}
+
 int check_key_ptr(const void* p) { return p ? PIR_OK : fail(PIR_EINVAL, "null key"); }
 
 const char* const kPhaseNames[] = {"key_prep", "tree_frontier", "tree_leaves", "scan",
@@ -303,6 +405,41 @@ int answer_dev_locked(pir_engine* e, const uint8_t* d_key, uint8_t* d_result, hi
   return PIR_OK;
 }
 
+int answer_batch_locked(pir_engine* e, const uint8_t* d_keys, int nk, uint8_t* d_result,
+                        hipStream_t s) {
+  const auto& c = e->cfg;
+  const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
+  e->ev = nullptr;
+  if (nk == 0) return PIR_OK;
+  if (c.is_byzantine) {
+    HIP_TRY(pir::launch_fill_random(d_result, out_bytes * nk, 0xB42u + (++e->byz_counter), s));
+    return PIR_OK;
+  }
+  if (nk == 1 || batch_group(e) == 1) {  // one key per shard pass: the single-query path
+    for (int q = 0; q < nk; ++q) {
+      int rc = answer_dev_locked(e, d_keys + (size_t)q * e->key_len, d_result + q * out_bytes, s);
+      if (rc) return rc;
+    }
+    return PIR_OK;
+  }
+  const size_t total = out_bytes * nk;
+  uint8_t* part_out = d_result;
+  if (e->comm) {
+    int rc = ensure_buf(&e->d_bpart, &e->bpart_cap, total);
+    if (!rc) rc = ensure_buf(&e->d_bgather, &e->bgather_cap, total * e->nranks);
+    if (rc) return rc;
+    part_out = e->d_bpart;
+  }
+  int rc = answer_batch_core(e, d_keys, nk, c.log_num_partitions, (uint64_t)c.partition_index, 0,
+                             part_out, s);
+  if (rc) return rc;
+  if (e->comm) {
+    RCCL_TRY(ncclAllGather(e->d_bpart, e->d_bgather, total, ncclUint8, e->comm, s));
+    HIP_TRY(pir::launch_xor_fold(e->d_bgather, e->nranks, total, d_result, s));
+  }
+  return PIR_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -351,6 +488,10 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
   if (hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail(PIR_EHIP, "hipEventCreate failed"));
+  for (int i = 0; i < 2; ++i)
+    if (hipEventCreateWithFlags(&e->ev_cb_ready[i], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_cb_free[i], hipEventDisableTiming) != hipSuccess)
+      return cleanup(fail(PIR_EHIP, "hipEventCreate failed"));
   pir::upload_aes_table(e->stream);
   const size_t shard_bytes = (size_t)e->rows * e->pitch;
   if (hipMalloc(&e->d_shard, shard_bytes) != hipSuccess)
@@ -361,6 +502,8 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
   {
     const char* f = getenv("PIR_FUSED");
     e->allow_fused = !(f && f[0] == '0');
+    const char* bg = getenv("PIR_BATCH_G");
+    if (bg) e->batch_group = atoi(bg);
     const int tile = pir::fused_tile(c.num_rounds, e->pitch, e->rows, e->num_cus);
     if (tile) {
       const pir::TreePlan pf =
@@ -395,7 +538,9 @@ void pir_engine_destroy(pir_engine_t* e) {
   for (auto* p : {(void*)e->d_shard, (void*)e->d_key_raw, (void*)e->d_keys,
                   (void*)e->nodes.s[0], (void*)e->nodes.s[1], (void*)e->nodes.t[0],
                   (void*)e->nodes.t[1], (void*)e->d_c, (void*)e->d_slabs, (void*)e->d_part,
-                  (void*)e->d_gather, (void*)e->d_result})
+                  (void*)e->d_gather, (void*)e->d_result, (void*)e->d_cb, (void*)e->d_gtmp,
+                  (void*)e->d_bpart, (void*)e->d_bgather, (void*)e->bnodes.s[0],
+                  (void*)e->bnodes.s[1], (void*)e->bnodes.t[0], (void*)e->bnodes.t[1]})
     if (p) (void)hipFree(p);
   for (auto& b : e->user) (void)hipFree(b.p);
   if (e->h_key) (void)hipHostFree(e->h_key);
@@ -404,6 +549,10 @@ void pir_engine_destroy(pir_engine_t* e) {
     for (auto& ev : sl.ev) (void)hipEventDestroy(ev);
   for (auto& ev : e->ev_leaf)
     if (ev) (void)hipEventDestroy(ev);
+  for (int i = 0; i < 2; ++i) {
+    if (e->ev_cb_ready[i]) (void)hipEventDestroy(e->ev_cb_ready[i]);
+    if (e->ev_cb_free[i]) (void)hipEventDestroy(e->ev_cb_free[i]);
+  }
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   if (e->aux) (void)hipStreamDestroy(e->aux);
@@ -485,13 +634,44 @@ int pir_engine_answer_batch_dev(pir_engine_t* e, const uint8_t* d_keys, int num_
   std::lock_guard<std::mutex> lk(e->mu);
   HIP_TRY(hipSetDevice(e->cfg.device));
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  return answer_batch_locked(e, d_keys, num_keys, d_result, s);
+}
+
+int pir_engine_answer_batch(pir_engine_t* e, const uint8_t* keys, int num_keys,
+                            uint8_t* results) {
+  if (!e || (num_keys > 0 && (!keys || !results)) || num_keys < 0)
+    return fail(PIR_EINVAL, "bad argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
   const size_t out_bytes = (size_t)e->cfg.num_rounds * e->cfg.record_bytes;
-  for (int q = 0; q < num_keys; ++q) {
-    int rc = answer_dev_locked(e, d_keys + (size_t)q * e->key_len, d_result + q * out_bytes, s);
-    if (rc) return rc;
+  const size_t kb = (size_t)num_keys * e->key_len, rb = (size_t)num_keys * out_bytes;
+  if (num_keys == 0) return PIR_OK;
+  uint8_t *d_k = nullptr, *d_r = nullptr;
+  HIP_TRY(hipMalloc(&d_k, kb));
+  if (hipMalloc(&d_r, rb) != hipSuccess) {
+    (void)hipFree(d_k);
+    return fail(PIR_ENOMEM, "batch result buffer %zu bytes", rb);
   }
+  int rc = PIR_OK;
+  if (hipMemcpyAsync(d_k, keys, kb, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+    rc = fail(PIR_EHIP, "key upload");
+  if (!rc) rc = answer_batch_locked(e, d_k, num_keys, d_r, e->stream);
+  if (!rc && (hipMemcpyAsync(results, d_r, rb, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+              hipStreamSynchronize(e->stream) != hipSuccess))
+    rc = fail(PIR_EHIP, "batch answer: %s", hipGetErrorString(hipGetLastError()));
+  (void)hipStreamSynchronize(e->stream);
+  (void)hipFree(d_k);
+  (void)hipFree(d_r);
+  return rc;
+}
+
+int pir_engine_set_batch_group(pir_engine_t* e, int keys_per_pass) {
+  if (!e || keys_per_pass < 0 || keys_per_pass > 16) return fail(PIR_EINVAL, "bad argument");
+  e->batch_group = keys_per_pass;
   return PIR_OK;
 }
+
+int pir_engine_batch_group(const pir_engine_t* e) { return e ? batch_group(e) : 0; }
 
 int pir_engine_answer(pir_engine_t* e, const uint8_t* key, uint8_t* result) {
   if (!e || !result) return fail(PIR_EINVAL, "null argument");

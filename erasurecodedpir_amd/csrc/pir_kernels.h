@@ -62,11 +62,17 @@ struct KeySrc {
   int p, n, nq, party0;
   DevKey* key;
 };
+// nkeys > 1: a batch of keys (raw keys raw_stride bytes apart, parsed keys ks.key[y], node
+// ranges node_stride nodes apart), one grid row per key
 hipError_t launch_frontier(const TreePlan& pl, const KeySrc& ks, const NodeBufs& nb,
-                           hipStream_t s);
-// expand stages [i0, i1) (i1 < 0: to the last) for chunk j of C of every stage's input range
+                           hipStream_t s, int nkeys = 1, size_t raw_stride = 0,
+                           uint64_t node_stride = 0);
+// expand stages [i0, i1) (i1 < 0: to the last) for chunk j of C of every stage's input range;
+// the final stage writes leaf i's nrp share bytes at d_c + i * cstride (cstride <= 0: nrp)
 hipError_t launch_stages(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb, int j, int C,
-                         uint8_t* d_c, int nrp, hipStream_t s, int i0 = 0, int i1 = -1);
+                         uint8_t* d_c, int nrp, hipStream_t s, int i0 = 0, int i1 = -1,
+                         int cstride = 0, int nkeys = 1, uint64_t node_stride = 0,
+                         uint32_t c_key_off = 0);
 // scan rows [0, nrec) of `shard` (row pitch `pitch`) with coefficients cT[i*nrp + a]
 struct ScanShape {
   int nq, nrp, vec;      // vec = dwords per lane chunk (4, 2, 1)

@@ -1,14 +1,16 @@
 // pir_kernels.hip -- CDNA4 (gfx950) kernels of the tree-DPF PIR answer path.
 //
-//   k_key_prep      raw genOptimizedDPF key bytes -> DevKey           (dpf_tree.cpp:504-519)
-//   k_tree_frontier root (or partition prefix) -> frontier level F    (dpf_tree.cpp:525-559)
-//   k_tree_leaves   frontier -> leaves -> DPF shares c[i][a]          (dpf_tree.cpp:525-580)
-//   k_scan          ans[a] ^= c[i][a] * shard[i]  over GF(2^8)        (server.cpp:121-127)
-//   k_reduce        XOR of per-workgroup partial answers              (server.cpp:553-562)
+//   k_key_prep   raw genOptimizedDPF key bytes -> DevKey               (dpf_tree.cpp:504-519)
+//   k_frontier   root (or partition prefix) -> frontier level F        (dpf_tree.cpp:525-559)
+//   k_expand     frontier -> ... -> leaves -> DPF shares c[i][a]       (dpf_tree.cpp:525-580)
+//   k_scan       ans[a] ^= c[i][a] * shard[i]  over GF(2^8)            (server.cpp:121-127)
+//   k_fused      leaf stage + scan in one persistent kernel (shares stay in LDS)
+//   k_reduce     XOR of per-workgroup partial answers                  (server.cpp:553-562)
+// k_frontier and k_expand take a batch of keys along gridDim.y (batched answers).
 //
 // AES-128 (the PRG G of utils.cpp:37-51 re-keys on every node seed) is a T-table cipher:
-// one 1 KiB table Te0 replicated 32x in LDS ([entry][lane & 31]) so every lane of a
-// 32-lane ds_read_b32 group hits its own bank; Te1..Te3 are byte rotations of Te0.
+// Te0 and Te2 = rotl16(Te0) replicated 32x in LDS (pir_aes.h) so every lane of a 32-lane
+// ds_read_b32 group hits its own bank; Te1, Te3 are byte rotations of Te0, Te2.
 // The GF(2^8) scan keeps, per lane, 8 bit-plane accumulators Z_k (Z_k ^= x when bit k of the
 // record's coefficient is set) and folds ans = sum_k alpha^k Z_k once at the end, so the
 // HBM stream costs ~1 VALU op per byte.
@@ -134,10 +136,18 @@ __device__ __forceinline__ uint32_t word_of(const uint4& v, uint32_t q) {
 __global__ __launch_bounds__(kFrontThreads) void k_frontier(
     const uint8_t* __restrict__ raw, int p, int n, int nq, int party0, DevKey* __restrict__ K,
     uint64_t prefix, int log_parts, int g, int e, uint4* __restrict__ out_s,
-    uint32_t* __restrict__ out_t) {
+    uint32_t* __restrict__ out_t, uint32_t raw_stride, uint64_t out_stride) {
   // raw != nullptr: parse the key here (every workgroup stages the CWs it needs in LDS;
   // workgroup 0 also writes the full DevKey for the later kernels).  raw == nullptr: K was
-  // written by k_key_prep.
+  // written by k_key_prep.  blockIdx.y = key of a batch (raw_stride bytes, K + y, out_stride
+  // nodes apart).
+  // latency-bound chain of dependent AES levels: issue ahead of throughput kernels that
+  // share the CU (the scan of the previous key group runs beside the frontier when batching)
+  __builtin_amdgcn_s_setprio(3);
+  if (raw) raw += (size_t)blockIdx.y * raw_stride;
+  K += blockIdx.y;
+  out_s += blockIdx.y * out_stride;
+  out_t += blockIdx.y * out_stride;
   __shared__ FrontSmem sm;
   __shared__ uint4 root_seed;
   __shared__ uint32_t root_t;
@@ -277,9 +287,12 @@ __device__ __forceinline__ void expand_node(const Tab& T, const DevKey* __restri
   tr = (tb >> B.pm1) & B.tmask;
 }
 
+// NRP bytes of leaf `leaf` at c + leaf * cstride (cstride = NRP, or a multiple of it when the
+// shares of several keys are interleaved per leaf for a batched scan)
 template <int NRP>
-__device__ __forceinline__ void store_leaf(uint8_t* __restrict__ c, uint64_t leaf, uint4 v) {
-  uint8_t* dst = c + leaf * NRP;
+__device__ __forceinline__ void store_leaf(uint8_t* __restrict__ c, uint64_t leaf, uint4 v,
+                                           uint32_t cstride = NRP) {
+  uint8_t* dst = c + leaf * cstride;
   if constexpr (NRP == 1) *dst = (uint8_t)v.x;
   else if constexpr (NRP == 2) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)v.x;
   else if constexpr (NRP == 4) *reinterpret_cast<uint32_t*>(dst) = v.x;
@@ -301,7 +314,15 @@ template <bool FINAL, int NRP>
 __global__ __launch_bounds__(kExpThreads) void k_expand(
     const DevKey* __restrict__ K, const uint4* __restrict__ in_s, const uint32_t* __restrict__ in_t,
     int L0, int k, int tile, uint4* __restrict__ out_s, uint32_t* __restrict__ out_t,
-    uint8_t* __restrict__ c) {
+    uint8_t* __restrict__ c, uint32_t cstride, uint64_t in_stride, uint64_t out_stride,
+    uint32_t c_key_off) {
+  // blockIdx.y = key of a batch: its DevKey, node ranges and share slot
+  K += blockIdx.y;
+  in_s += blockIdx.y * in_stride;
+  in_t += blockIdx.y * in_stride;
+  out_s += blockIdx.y * out_stride;
+  out_t += blockIdx.y * out_stride;
+  c += (size_t)blockIdx.y * c_key_off;
   constexpr int NW = NRP <= 4 ? 1 : NRP / 4;
   __shared__ ExpSmem sm;
   load_tables(sm.tab);
@@ -323,7 +344,7 @@ __global__ __launch_bounds__(kExpThreads) void k_expand(
     __syncthreads();
     for (int i = threadIdx.x; i < tile; i += blockDim.x) {
       const uint4 v = leaf_value<NW>(T, K, B.pm1, in_s[ibase + i], in_t[ibase + i]);
-      store_leaf<NRP>(c, obase + i, make_uint4(v.x & qm.x, v.y & qm.y, v.z & qm.z, v.w & qm.w));
+      store_leaf<NRP>(c, obase + i, make_uint4(v.x & qm.x, v.y & qm.y, v.z & qm.z, v.w & qm.w), cstride);
     }
     return;
   }
@@ -365,12 +386,12 @@ __global__ __launch_bounds__(kExpThreads) void k_expand(
     if constexpr (FINAL) {
       const uint4 vl = leaf_value<NW>(T, K, B.pm1, sl, tl);
       const uint4 vr = leaf_value<NW>(T, K, B.pm1, sr, tr);
-      if constexpr (NRP == 1) {  // both leaves in one 16-bit store
+      if (NRP == 1 && cstride == 1) {  // both leaves in one 16-bit store
         *reinterpret_cast<uint16_t*>(c + obase + 2 * u) =
             (uint16_t)((vl.x & qm.x & 0xffu) | ((vr.x & qm.x & 0xffu) << 8));
       } else {
-        store_leaf<NRP>(c, obase + 2 * u, make_uint4(vl.x & qm.x, vl.y & qm.y, vl.z & qm.z, vl.w & qm.w));
-        store_leaf<NRP>(c, obase + 2 * u + 1, make_uint4(vr.x & qm.x, vr.y & qm.y, vr.z & qm.z, vr.w & qm.w));
+        store_leaf<NRP>(c, obase + 2 * u, make_uint4(vl.x & qm.x, vl.y & qm.y, vl.z & qm.z, vl.w & qm.w), cstride);
+        store_leaf<NRP>(c, obase + 2 * u + 1, make_uint4(vr.x & qm.x, vr.y & qm.y, vr.z & qm.z, vr.w & qm.w), cstride);
       }
     } else {
       out_s[obase + 2 * u] = sl;
@@ -1007,37 +1028,52 @@ hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys
 }
 
 hipError_t launch_frontier(const TreePlan& pl, const KeySrc& ks, const NodeBufs& nb,
-                           hipStream_t s) {
+                           hipStream_t s, int nkeys, size_t raw_stride, uint64_t node_stride) {
   const int nlev = pl.log_parts + pl.g + pl.e;
   const uint8_t* raw = ks.raw;
   if (raw && nlev > kFrontCwLevels) {  // CWs read from global: parse in a kernel of its own
-    hipError_t err = launch_key_prep(raw, 0, 1, ks.p, ks.n, ks.nq, ks.party0, ks.key, s);
+    hipError_t err = launch_key_prep(raw, raw_stride, nkeys, ks.p, ks.n, ks.nq, ks.party0,
+                                     ks.key, s);
     if (err != hipSuccess) return err;
     raw = nullptr;
   }
-  hipLaunchKernelGGL(k_frontier, dim3(1u << pl.g), dim3(kFrontThreads), 0, s, raw, ks.p, ks.n,
-                     ks.nq, ks.party0, ks.key, pl.prefix, pl.log_parts, pl.g, pl.e, nb.s[0],
-                     nb.t[0]);
+  hipLaunchKernelGGL(k_frontier, dim3(1u << pl.g, nkeys), dim3(kFrontThreads), 0, s, raw, ks.p,
+                     ks.n, ks.nq, ks.party0, ks.key, pl.prefix, pl.log_parts, pl.g, pl.e,
+                     nb.s[0], nb.t[0], (uint32_t)raw_stride, node_stride);
   return hipGetLastError();
 }
+
+struct BatchDims {
+  int nkeys;
+  uint64_t node_stride;  // nodes between the keys' node ranges
+  uint32_t c_key_off;    // bytes between the keys' share slots
+};
 
 template <int NRP>
 static hipError_t launch_stage(const Stage& st, const DevKey* d_key, const uint4* is,
                                const uint32_t* it, uint4* os, uint32_t* ot, uint8_t* c,
-                               unsigned blocks, hipStream_t s) {
+                               uint32_t cstride, unsigned blocks, const BatchDims& bd,
+                               hipStream_t s) {
+  const dim3 grid(blocks, bd.nkeys);
   if (st.final)
-    hipLaunchKernelGGL((k_expand<true, NRP>), dim3(blocks), dim3(kExpThreads), 0, s, d_key, is,
-                       it, st.L_in, st.k, st.tile, os, ot, c);
+    hipLaunchKernelGGL((k_expand<true, NRP>), grid, dim3(kExpThreads), 0, s, d_key, is, it,
+                       st.L_in, st.k, st.tile, os, ot, c, cstride, bd.node_stride,
+                       bd.node_stride, bd.c_key_off);
   else
-    hipLaunchKernelGGL((k_expand<false, 1>), dim3(blocks), dim3(kExpThreads), 0, s, d_key, is,
-                       it, st.L_in, st.k, st.tile, os, ot, c);
+    hipLaunchKernelGGL((k_expand<false, 1>), grid, dim3(kExpThreads), 0, s, d_key, is, it,
+                       st.L_in, st.k, st.tile, os, ot, c, cstride, bd.node_stride,
+                       bd.node_stride, bd.c_key_off);
   return hipGetLastError();
 }
 
-// stages [i0, i1) of chunk j of C (each stage's input range split evenly)
+// stages [i0, i1) of chunk j of C (each stage's input range split evenly); the final stage
+// writes leaf i's nrp share bytes at d_c + i * cstride (cstride <= 0: nrp)
 hipError_t launch_stages(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb, int j, int C,
-                         uint8_t* d_c, int nrp, hipStream_t s, int i0s, int i1s) {
+                         uint8_t* d_c, int nrp, hipStream_t s, int i0s, int i1s, int cstride,
+                         int nkeys, uint64_t node_stride, uint32_t c_key_off) {
   if (i1s < 0) i1s = pl.nstages;
+  const uint32_t cs = cstride > 0 ? (uint32_t)cstride : (uint32_t)nrp;
+  const BatchDims bd{nkeys, node_stride, c_key_off};
   for (int i = i0s; i < i1s; ++i) {
     const Stage& st = pl.st[i];
     const uint64_t nin = st.nin / C, i0 = nin * j, o0 = i0 << st.k;
@@ -1045,15 +1081,15 @@ hipError_t launch_stages(const TreePlan& pl, const DevKey* d_key, const NodeBufs
     const uint32_t* it = nb.t[i & 1] + i0;
     uint4* os = nb.s[(i + 1) & 1] + o0;
     uint32_t* ot = nb.t[(i + 1) & 1] + o0;
-    uint8_t* c = d_c + o0 * nrp;
+    uint8_t* c = d_c + o0 * cs;
     const unsigned blocks = (unsigned)(nin / st.tile);
     hipError_t e;
     switch (nrp) {
-      case 1: e = launch_stage<1>(st, d_key, is, it, os, ot, c, blocks, s); break;
-      case 2: e = launch_stage<2>(st, d_key, is, it, os, ot, c, blocks, s); break;
-      case 4: e = launch_stage<4>(st, d_key, is, it, os, ot, c, blocks, s); break;
-      case 8: e = launch_stage<8>(st, d_key, is, it, os, ot, c, blocks, s); break;
-      case 16: e = launch_stage<16>(st, d_key, is, it, os, ot, c, blocks, s); break;
+      case 1: e = launch_stage<1>(st, d_key, is, it, os, ot, c, cs, blocks, bd, s); break;
+      case 2: e = launch_stage<2>(st, d_key, is, it, os, ot, c, cs, blocks, bd, s); break;
+      case 4: e = launch_stage<4>(st, d_key, is, it, os, ot, c, cs, blocks, bd, s); break;
+      case 8: e = launch_stage<8>(st, d_key, is, it, os, ot, c, cs, blocks, bd, s); break;
+      case 16: e = launch_stage<16>(st, d_key, is, it, os, ot, c, cs, blocks, bd, s); break;
       default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;
@@ -1073,6 +1109,10 @@ ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus) {
   sh.nq = nq;
   sh.nrp = nq == 1 ? 1 : (nq == 2 ? 2 : (nq <= 4 ? 4 : (nq <= 8 ? 8 : 16)));
   sh.vec = vec_for(nq);
+  // a record narrower than a VEC=2 wave row but at least a VEC=1 row: one record per row
+  // (wave-uniform coefficients, SGPR masks) beats per-lane coefficients for several records
+  if (sh.vec == 2 && pitch / 8 < (uint32_t)kColGroupLanes && pitch / 4 >= (uint32_t)kColGroupLanes)
+    sh.vec = 1;
   sh.pitch = pitch;
   sh.cpr = pitch / (sh.vec * 4);
   sh.uniform = sh.cpr >= (uint32_t)kColGroupLanes;
@@ -1093,6 +1133,14 @@ static hipError_t scan_nq(const ScanShape& sh, const uint8_t* d_shard, uint64_t 
                           const uint8_t* d_c, uint8_t* d_slabs, int acc, hipStream_t s) {
   constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : (NQ <= 8 ? 8 : 16)));
   constexpr int VEC = NQ <= 2 ? 4 : (NQ <= 8 ? 2 : 1);
+  if constexpr (VEC == 2) {
+    if (sh.vec == 1) {
+      if (!sh.uniform) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((k_scan<NQ, NRP, 1, true>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
+                         nrec, sh.pitch, sh.cpr, d_c, d_slabs, acc);
+      return hipGetLastError();
+    }
+  }
   if (sh.uniform)
     hipLaunchKernelGGL((k_scan<NQ, NRP, VEC, true>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
                        nrec, sh.pitch, sh.cpr, d_c, d_slabs, acc);

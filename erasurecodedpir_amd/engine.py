@@ -107,6 +107,31 @@ class Engine:
               "pir_engine_answer")
         return out
 
+    def answer_batch(self, keys):
+        """(num_keys, num_rounds, record_bytes) answers of keys (a sequence of key_len-byte
+        keys, or a (num_keys, key_len) uint8 array), batch_group keys per shard pass."""
+        ks = [_buf(k)[0] for k in keys]
+        for k in ks:
+            if k.size != self.key_len:
+                raise ValueError(f"key of {k.size} bytes, expected {self.key_len}")
+        nk = len(ks)
+        flat = np.ascontiguousarray(np.concatenate(ks) if nk else np.zeros(0, np.uint8),
+                                    dtype=np.uint8)
+        out = np.empty((nk, self.num_rounds, self.record_bytes), np.uint8)
+        check(self._lib.pir_engine_answer_batch(self._h, flat.ctypes.data_as(ctypes.c_void_p), nk,
+                                                out.ctypes.data_as(ctypes.c_void_p)),
+              "pir_engine_answer_batch")
+        return out
+
+    @property
+    def batch_group(self):
+        """Keys answered per pass over the shard."""
+        return self._lib.pir_engine_batch_group(self._h)
+
+    @batch_group.setter
+    def batch_group(self, g):
+        check(self._lib.pir_engine_set_batch_group(self._h, int(g)), "set_batch_group")
+
     def answer_slice(self, key, thread_num, num_threads):
         k, kp = self._check_key(key)
         out = np.empty((self.num_rounds, self.record_bytes), np.uint8)

@@ -86,9 +86,18 @@ int pir_engine_eval_all(pir_engine_t *e, const uint8_t *key, uint8_t *out);
  *      engine's own stream) ---- */
 int pir_engine_answer_dev(pir_engine_t *e, const uint8_t *d_key, uint8_t *d_result,
                           void *stream);
-/* `num_keys` keys of key_len bytes back to back; results num_keys x num_rounds x record_bytes */
+/* `num_keys` keys of key_len bytes back to back; results num_keys x num_rounds x record_bytes.
+ * Keys are answered in groups of pir_engine_batch_group() keys per pass over the shard (the
+ * shard is read once per group, each key's tree is evaluated separately). */
 int pir_engine_answer_batch_dev(pir_engine_t *e, const uint8_t *d_keys, int num_keys,
                                 uint8_t *d_result, void *stream);
+/* host-buffer form of the above (synchronous) */
+int pir_engine_answer_batch(pir_engine_t *e, const uint8_t *keys, int num_keys,
+                            uint8_t *results);
+/* keys per shard pass: 0 = automatic (8 / nrp), else a power of two <= 16 / nrp, where nrp =
+ * num_rounds rounded up to a power of two.  Default from $PIR_BATCH_G. */
+int pir_engine_set_batch_group(pir_engine_t *e, int keys_per_pass);
+int pir_engine_batch_group(const pir_engine_t *e);
 void *pir_engine_stream(pir_engine_t *e);
 int pir_engine_sync(pir_engine_t *e);
 /* device scratch the caller may use for keys/results (freed with the engine) */

@@ -1,0 +1,109 @@
+"""Batched answers (BASELINE configs[2]: many keys against one shard pass): every key of a batch
+must get exactly the answer it gets alone -- the oracle's answer on the same key and shard --
+for every keys-per-pass grouping, ragged last groups, multi-round keys, partitions and the
+byzantine flag; at full size the 2-party PIR property holds for every key of the batch."""
+import numpy as np
+import pytest
+
+import _oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pir():
+    import erasurecodedpir_amd as pir
+    pir.load()
+    return pir
+
+
+def _keys(p, n, nq, idxs, rng):
+    fcw = O.final_cw(p, nq, 1)
+    out = []
+    for idx in idxs:
+        seeds = rng.integers(0, 256, 16 * p, dtype=np.uint8).tobytes()
+        out.append(O.gen_keys(n, int(idx), fcw, p, nq, seeds))
+    return out  # [key index][party]
+
+
+BATCH_SHAPES = [  # (p, n, efs, nq, num_keys, keys per pass; 0 = automatic)
+    (2, 12, 256, 1, 13, 0), (2, 10, 96, 1, 8, 16), (2, 11, 1024, 1, 5, 4), (2, 9, 1, 1, 3, 2),
+    (3, 11, 100, 3, 5, 0), (3, 10, 48, 2, 9, 8), (5, 9, 48, 4, 7, 4), (8, 10, 64, 5, 3, 2),
+    (8, 10, 64, 5, 3, 0), (2, 13, 4096, 1, 4, 8), (17, 8, 40, 16, 2, 0), (9, 9, 32, 1, 17, 16),
+]
+
+
+@pytest.mark.parametrize("shape", BATCH_SHAPES, ids=lambda s: "p%d_n%d_efs%d_nq%d_k%d_g%d" % s)
+def test_batch_vs_oracle(pir, shape):
+    p, n, efs, nq, nk, g = shape
+    rng = np.random.default_rng(hash(shape) & 0xFFFF)
+    idxs = rng.integers(0, 1 << n, nk)
+    keys = _keys(p, n, nq, idxs, rng)
+    shard = rng.integers(0, 256, (1 << n) * efs, dtype=np.uint8)
+    party = int(rng.integers(0, p))
+    with pir.Engine(p, party + 1, n, efs, nq) as e:
+        e.set_shard(shard)
+        e.batch_group = g
+        got = e.answer_batch([k[party] for k in keys])
+        single = e.answer(keys[-1][party])
+    assert got.shape == (nk, nq, efs)
+    for q in range(nk):
+        want = O.answer(p, party + 1, n, efs, nq, keys[q][party], shard)
+        assert np.array_equal(got[q], want), q
+    assert np.array_equal(got[-1], single)
+
+
+def test_batch_empty_and_single(pir):
+    p, n, efs, nq = 2, 8, 64, 1
+    rng = np.random.default_rng(5)
+    keys = _keys(p, n, nq, [17], rng)
+    shard = rng.integers(0, 256, (1 << n) * efs, dtype=np.uint8)
+    with pir.Engine(p, 1, n, efs, nq) as e:
+        e.set_shard(shard)
+        assert e.answer_batch([]).shape == (0, nq, efs)
+        one = e.answer_batch([keys[0][0]])
+    assert np.array_equal(one[0], O.answer(p, 1, n, efs, nq, keys[0][0], shard))
+
+
+def test_batch_partitions_xor_to_full(pir):
+    p, n, efs, nq, nk = 2, 12, 256, 1, 6
+    rng = np.random.default_rng(11)
+    keys = [k[0] for k in _keys(p, n, nq, rng.integers(0, 1 << n, nk), rng)]
+    shard = rng.integers(0, 256, ((1 << n), efs), dtype=np.uint8)
+    with pir.Engine(p, 1, n, efs, nq) as e:
+        e.set_shard(shard)
+        full = e.answer_batch(keys)
+    acc = np.zeros_like(full)
+    rows = (1 << n) >> 2
+    for part in range(4):
+        with pir.Engine(p, 1, n, efs, nq, log_num_partitions=2, partition_index=part) as e:
+            e.set_shard(shard[part * rows:(part + 1) * rows])
+            acc ^= e.answer_batch(keys)
+    assert np.array_equal(acc, full)
+
+
+def test_batch_byzantine_random(pir):
+    p, n, efs, nq = 2, 6, 64, 1
+    keys = pir.gen_keys(n, 3, p, nq)
+    with pir.Engine(p, 1, n, efs, nq, is_byzantine=True) as e:
+        a = e.answer_batch([keys[0]] * 4)
+    assert a.shape == (4, nq, efs) and not np.array_equal(a[0], a[1])
+
+
+def test_batch_pir_property_full_size(pir):
+    """configs[2] shape scaled to 2^20 x 256 B, 32 keys: per key ans1 ^ ans2 = finalCW * record."""
+    p, nq, n, efs, nk = 2, 1, 20, 256, 32
+    fcw = O.final_cw(p, nq, 1)
+    rng = np.random.default_rng(3)
+    idxs = [int(i) for i in rng.integers(0, 1 << n, nk)]
+    keys = [pir.gen_keys(n, i, p, nq, fcw=fcw) for i in idxs]
+    ans = []
+    recs = None
+    for party in range(p):
+        with pir.Engine(p, party + 1, n, efs, nq) as e:
+            e.fill_shard_random(0xBA7C4)
+            recs = [e.shard_row(i) for i in idxs]
+            ans.append(e.answer_batch([k[party] for k in keys]))
+    table = np.array([O.gf_mul(int(fcw[0]), x) for x in range(256)], np.uint8)
+    for q in range(nk):
+        assert np.array_equal(ans[0][q][0] ^ ans[1][q][0], table[recs[q]]), q
