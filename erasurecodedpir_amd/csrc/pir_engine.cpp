@@ -66,6 +66,8 @@ struct DevBuf {
 // Event layout of one profiled answer.  Leaves and scans run as kMaxChunks-way pipelined
 // chunks on two streams (tree leaves of chunk j+1 overlap the shard scan of chunk j).
 constexpr int kMaxChunks = 8;
+constexpr int kFrontBatch = 256;  // batched answers: keys whose upper tree levels run together
+constexpr uint64_t kBatchNodeBytes = 4ull << 30;  // ... within this much node memory
 enum {
   EV_START = 0, EV_KEY = 1, EV_FRONT = 2,
   EV_LEAF_B = 3, EV_LEAF_E = EV_LEAF_B + kMaxChunks,
@@ -101,7 +103,7 @@ struct pir_engine {
   // batched answers: interleaved shares of a key group, group answer, batch partition answer
   uint8_t* d_cb = nullptr;
   size_t cb_cap = 0;
-  pir::NodeBufs bnodes{};       // node buffers of a key group (G x max_nodes)
+  pir::NodeBufs bnodes{};       // upper tree levels of a batch's super-group (FB x max_nodes)
   uint64_t bnodes_cap = 0;
   uint8_t* d_gtmp = nullptr;    // 16*efs
   uint8_t* d_bpart = nullptr;   // batch partition answers (split shard)
@@ -109,6 +111,7 @@ struct pir_engine {
   size_t bpart_cap = 0, bgather_cap = 0;
   int batch_group = 0;          // keys per shard pass (0: automatic; $PIR_BATCH_G)
   int last_batch_group = 0;
+  int batch_scan_bpc = 2;       // scan workgroups per CU in batched answers ($PIR_BATCH_SCAN_BPC)
   uint8_t* d_result = nullptr;  // nq*efs (host-API staging)
   uint8_t* h_key = nullptr;     // pinned
   uint8_t* h_res = nullptr;     // pinned
@@ -148,6 +151,24 @@ int ensure_buf(uint8_t** p, size_t* cap, size_t bytes) {
   *cap = 0;
   HIP_TRY(hipMalloc(p, bytes));
   *cap = bytes;
+  return PIR_OK;
+}
+
+// nb.s/t[0..nbuf) with room for `nodes` nodes each
+int ensure_nodes(pir::NodeBufs* nb, uint64_t* cap, uint64_t nodes, int nbuf) {
+  if (nodes <= *cap) return PIR_OK;
+  for (int i = 0; i < 2; ++i) {
+    if (nb->s[i]) (void)hipFree(nb->s[i]);
+    if (nb->t[i]) (void)hipFree(nb->t[i]);
+    nb->s[i] = nullptr;
+    nb->t[i] = nullptr;
+  }
+  *cap = 0;
+  for (int i = 0; i < nbuf; ++i) {
+    HIP_TRY(hipMalloc(&nb->s[i], nodes * sizeof(uint4)));
+    HIP_TRY(hipMalloc(&nb->t[i], nodes * sizeof(uint32_t)));
+  }
+  *cap = nodes;
   return PIR_OK;
 }
 
@@ -260,12 +281,15 @@ int batch_group(const pir_engine* e) {
 }
 
 // nk keys (raw, key_len apart) against one partition slice, one shard pass per group of G
-// keys: each key's tree (frontier + stages) writes its shares into slot g of the interleaved
-// coefficient rows cb[i][G*nrp]; one multi-round scan of G*nrp rounds answers the group
-// (round g*nrp + a = key g, round a).  d_out: nk x nq x efs.
-//   s  : trees of group j into share buffer j%2   (waits until scan j-2 has read it)
-//   aux: scan + reduce of group j                  (after the trees of group j)
-// so the trees of group j+1 run beside the scan of group j.
+// keys: each key's tree writes its shares into slot g of the interleaved coefficient rows
+// cb[i][G*nrp]; one multi-round scan of G*nrp rounds answers the group (round g*nrp + a =
+// key g, round a).  d_out: nk x nq x efs.
+//   s  : per super-group of FB keys: frontier + all but the last tree stage of the FB keys
+//        (one launch per stage, keys along grid y); then per group of G keys the last
+//        (leaf) stage into share buffer j%2 (after scan j-2 has read it)
+//   aux: scan + reduce of group j (after its leaf stage)
+// so the leaf stage of group j+1 runs beside the scan of group j.  (Node-writing stages beside
+// a scan are starved of the CU's memory pipeline, hence the up-front upper stages.)
 int answer_batch_core(pir_engine* e, const uint8_t* d_raw, int nk, int log_parts_total,
                       uint64_t prefix, uint64_t row0, uint8_t* d_out, hipStream_t s) {
   const auto& c = e->cfg;
@@ -275,41 +299,46 @@ int answer_batch_core(pir_engine* e, const uint8_t* d_raw, int nk, int log_parts
   e->last_fused = 0;
   e->last_chunks = 1;
   const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix);
-  const pir::ScanShape sh = pir::make_scan_shape(pl.nleaves, e->pitch, W, e->num_cus);
+  const pir::ScanShape sh =
+      pir::make_scan_shape(pl.nleaves, e->pitch, W, e->num_cus, e->batch_scan_bpc);
   const size_t cb_bytes = (size_t)pl.nleaves * W;
+  // super-group: as many keys as kBatchNodeBytes of upper-level nodes hold (a multiple of G)
+  const uint64_t per_key = 2 * pl.max_nodes * (sizeof(uint4) + sizeof(uint32_t));
+  int FB = (int)std::min<uint64_t>(kFrontBatch, std::max<uint64_t>(1, kBatchNodeBytes / per_key));
+  FB = std::max(G, FB / G * G);
+  const int nsg = std::min(nk, FB);
   int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
   if (!rc) rc = ensure_buf(&e->d_cb, &e->cb_cap, 2 * cb_bytes);
   if (!rc) rc = ensure_batch(e, nk);
+  if (!rc) rc = ensure_nodes(&e->bnodes, &e->bnodes_cap, (uint64_t)nsg * pl.max_nodes, 2);
   if (rc) return rc;
   if (!e->d_gtmp) HIP_TRY(hipMalloc(&e->d_gtmp, (size_t)16 * c.record_bytes));
-  const uint64_t need_nodes = (uint64_t)G * pl.max_nodes;
-  if (need_nodes > e->bnodes_cap) {
-    for (int i = 0; i < 2; ++i) {
-      if (e->bnodes.s[i]) (void)hipFree(e->bnodes.s[i]);
-      if (e->bnodes.t[i]) (void)hipFree(e->bnodes.t[i]);
-      e->bnodes.s[i] = nullptr;
-      e->bnodes.t[i] = nullptr;
-    }
-    e->bnodes_cap = 0;
-    for (int i = 0; i < 2; ++i) {
-      HIP_TRY(hipMalloc(&e->bnodes.s[i], need_nodes * sizeof(uint4)));
-      HIP_TRY(hipMalloc(&e->bnodes.t[i], need_nodes * sizeof(uint32_t)));
-    }
-    e->bnodes_cap = need_nodes;
-  }
   const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
+  const int last = pl.nstages - 1;
   HIP_TRY(hipEventRecord(e->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(e->aux, e->ev_fork, 0));
   for (int q0 = 0, j = 0; q0 < nk; q0 += G, ++j) {
-    const int ng = std::min(G, nk - q0), b = j & 1;
+    const int ng = std::min(G, nk - q0), b = j & 1, r0 = q0 % FB;
+    if (r0 == 0) {  // frontier + upper stages of the next FB keys
+      const int nf = std::min(FB, nk - q0);
+      const pir::KeySrc ks{d_raw + (size_t)q0 * e->key_len, c.num_parties, c.log_num_records,
+                           c.num_rounds, c.party_index - 1, e->d_keys + q0};
+      HIP_TRY(pir::launch_frontier(pl, ks, e->bnodes, s, nf, (size_t)e->key_len, pl.max_nodes));
+      if (last > 0) {
+        const pir::StageBatch up{nf, pl.max_nodes, 0, nullptr, nullptr, 0};
+        HIP_TRY(pir::launch_stages(pl, e->d_keys + q0, e->bnodes, 0, 1, nullptr, e->nrp, s, 0,
+                                   last, 0, &up));
+      }
+    }
     uint8_t* cb = e->d_cb + b * cb_bytes;
     if (j >= 2) HIP_TRY(hipStreamWaitEvent(s, e->ev_cb_free[b], 0));
-    // the ng trees of the group side by side: grid row y = key q0 + y
-    const pir::KeySrc ks{d_raw + (size_t)q0 * e->key_len, c.num_parties, c.log_num_records,
-                         c.num_rounds, c.party_index - 1, e->d_keys + q0};
-    HIP_TRY(pir::launch_frontier(pl, ks, e->bnodes, s, ng, (size_t)e->key_len, pl.max_nodes));
-    HIP_TRY(pir::launch_stages(pl, e->d_keys + q0, e->bnodes, 0, 1, cb, e->nrp, s, 0, -1, W, ng,
-                               pl.max_nodes, (uint32_t)e->nrp));
+    // the leaf stage of the ng trees of the group side by side: grid row y = key q0 + y
+    const uint64_t off = (uint64_t)r0 * pl.max_nodes;
+    const pir::NodeBufs nbg{{e->bnodes.s[0] + off, e->bnodes.s[1] + off},
+                            {e->bnodes.t[0] + off, e->bnodes.t[1] + off}};
+    const pir::StageBatch sb{ng, pl.max_nodes, (uint32_t)e->nrp, nullptr, nullptr, 0};
+    HIP_TRY(pir::launch_stages(pl, e->d_keys + q0, nbg, 0, 1, cb, e->nrp, s, last, last + 1, W,
+                               &sb));
     HIP_TRY(hipEventRecord(e->ev_cb_ready[b], s));
     HIP_TRY(hipStreamWaitEvent(e->aux, e->ev_cb_ready[b], 0));
     // slots g >= ng hold stale shares: their rounds are computed and dropped
@@ -504,6 +533,8 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
     e->allow_fused = !(f && f[0] == '0');
     const char* bg = getenv("PIR_BATCH_G");
     if (bg) e->batch_group = atoi(bg);
+    const char* bb = getenv("PIR_BATCH_SCAN_BPC");
+    if (bb) e->batch_scan_bpc = std::max(1, atoi(bb));
     const int tile = pir::fused_tile(c.num_rounds, e->pitch, e->rows, e->num_cus);
     if (tile) {
       const pir::TreePlan pf =

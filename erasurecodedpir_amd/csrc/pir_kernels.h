@@ -62,6 +62,17 @@ struct KeySrc {
   int p, n, nq, party0;
   DevKey* key;
 };
+// A batch of keys expanded side by side (grid row y = key y): parsed keys d_key[y], node
+// ranges node_stride nodes apart in both ping-pong buffers, shares at d_c + y * c_key_off; the
+// first stage may read its input from a separate array (in0, in0_stride nodes per key).
+struct StageBatch {
+  int nkeys;
+  uint64_t node_stride;
+  uint32_t c_key_off;
+  const uint4* in0_s;
+  const uint32_t* in0_t;
+  uint64_t in0_stride;
+};
 // nkeys > 1: a batch of keys (raw keys raw_stride bytes apart, parsed keys ks.key[y], node
 // ranges node_stride nodes apart), one grid row per key
 hipError_t launch_frontier(const TreePlan& pl, const KeySrc& ks, const NodeBufs& nb,
@@ -71,8 +82,7 @@ hipError_t launch_frontier(const TreePlan& pl, const KeySrc& ks, const NodeBufs&
 // the final stage writes leaf i's nrp share bytes at d_c + i * cstride (cstride <= 0: nrp)
 hipError_t launch_stages(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb, int j, int C,
                          uint8_t* d_c, int nrp, hipStream_t s, int i0 = 0, int i1 = -1,
-                         int cstride = 0, int nkeys = 1, uint64_t node_stride = 0,
-                         uint32_t c_key_off = 0);
+                         int cstride = 0, const StageBatch* batch = nullptr);
 // scan rows [0, nrec) of `shard` (row pitch `pitch`) with coefficients cT[i*nrp + a]
 struct ScanShape {
   int nq, nrp, vec;      // vec = dwords per lane chunk (4, 2, 1)
@@ -81,7 +91,9 @@ struct ScanShape {
   uint32_t slab_bytes;   // per-workgroup partial = nq * 64 * vec * 4
   dim3 grid;
 };
-ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus);
+// blocks_per_cu <= 0: kScanBlocksPerCU.  One block per CU leaves room on every CU for a
+// 1024-thread tree workgroup beside the scan (batched answers overlap the two).
+ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus, int blocks_per_cu = 0);
 // accumulate: XOR into the slabs instead of overwriting them (chunked scans of one answer)
 hipError_t launch_scan(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
                        const uint8_t* d_c, uint8_t* d_slabs, bool accumulate, hipStream_t s);

@@ -141,9 +141,6 @@ __global__ __launch_bounds__(kFrontThreads) void k_frontier(
   // workgroup 0 also writes the full DevKey for the later kernels).  raw == nullptr: K was
   // written by k_key_prep.  blockIdx.y = key of a batch (raw_stride bytes, K + y, out_stride
   // nodes apart).
-  // latency-bound chain of dependent AES levels: issue ahead of throughput kernels that
-  // share the CU (the scan of the previous key group runs beside the frontier when batching)
-  __builtin_amdgcn_s_setprio(3);
   if (raw) raw += (size_t)blockIdx.y * raw_stride;
   K += blockIdx.y;
   out_s += blockIdx.y * out_stride;
@@ -1043,26 +1040,20 @@ hipError_t launch_frontier(const TreePlan& pl, const KeySrc& ks, const NodeBufs&
   return hipGetLastError();
 }
 
-struct BatchDims {
-  int nkeys;
-  uint64_t node_stride;  // nodes between the keys' node ranges
-  uint32_t c_key_off;    // bytes between the keys' share slots
-};
-
 template <int NRP>
 static hipError_t launch_stage(const Stage& st, const DevKey* d_key, const uint4* is,
                                const uint32_t* it, uint4* os, uint32_t* ot, uint8_t* c,
-                               uint32_t cstride, unsigned blocks, const BatchDims& bd,
-                               hipStream_t s) {
-  const dim3 grid(blocks, bd.nkeys);
+                               uint32_t cstride, unsigned blocks, int nkeys, uint64_t in_stride,
+                               uint64_t out_stride, uint32_t c_key_off, hipStream_t s) {
+  const dim3 grid(blocks, nkeys);
   if (st.final)
     hipLaunchKernelGGL((k_expand<true, NRP>), grid, dim3(kExpThreads), 0, s, d_key, is, it,
-                       st.L_in, st.k, st.tile, os, ot, c, cstride, bd.node_stride,
-                       bd.node_stride, bd.c_key_off);
+                       st.L_in, st.k, st.tile, os, ot, c, cstride, in_stride, out_stride,
+                       c_key_off);
   else
     hipLaunchKernelGGL((k_expand<false, 1>), grid, dim3(kExpThreads), 0, s, d_key, is, it,
-                       st.L_in, st.k, st.tile, os, ot, c, cstride, bd.node_stride,
-                       bd.node_stride, bd.c_key_off);
+                       st.L_in, st.k, st.tile, os, ot, c, cstride, in_stride, out_stride,
+                       c_key_off);
   return hipGetLastError();
 }
 
@@ -1070,28 +1061,38 @@ static hipError_t launch_stage(const Stage& st, const DevKey* d_key, const uint4
 // writes leaf i's nrp share bytes at d_c + i * cstride (cstride <= 0: nrp)
 hipError_t launch_stages(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb, int j, int C,
                          uint8_t* d_c, int nrp, hipStream_t s, int i0s, int i1s, int cstride,
-                         int nkeys, uint64_t node_stride, uint32_t c_key_off) {
+                         const StageBatch* batch) {
   if (i1s < 0) i1s = pl.nstages;
   const uint32_t cs = cstride > 0 ? (uint32_t)cstride : (uint32_t)nrp;
-  const BatchDims bd{nkeys, node_stride, c_key_off};
+  const int nkeys = batch ? batch->nkeys : 1;
+  const uint64_t stride = batch ? batch->node_stride : 0;
+  const uint32_t c_key_off = batch ? batch->c_key_off : 0;
   for (int i = i0s; i < i1s; ++i) {
     const Stage& st = pl.st[i];
     const uint64_t nin = st.nin / C, i0 = nin * j, o0 = i0 << st.k;
     const uint4* is = nb.s[i & 1] + i0;
     const uint32_t* it = nb.t[i & 1] + i0;
+    uint64_t in_stride = stride;
+    if (batch && batch->in0_s && i == i0s) {  // first stage input from a separate array
+      is = batch->in0_s + i0;
+      it = batch->in0_t + i0;
+      in_stride = batch->in0_stride;
+    }
     uint4* os = nb.s[(i + 1) & 1] + o0;
     uint32_t* ot = nb.t[(i + 1) & 1] + o0;
-    uint8_t* c = d_c + o0 * cs;
+    uint8_t* c = d_c ? d_c + o0 * cs : nullptr;
     const unsigned blocks = (unsigned)(nin / st.tile);
     hipError_t e;
+#define PIR_STAGE(N) launch_stage<N>(st, d_key, is, it, os, ot, c, cs, blocks, nkeys, in_stride, stride, c_key_off, s)
     switch (nrp) {
-      case 1: e = launch_stage<1>(st, d_key, is, it, os, ot, c, cs, blocks, bd, s); break;
-      case 2: e = launch_stage<2>(st, d_key, is, it, os, ot, c, cs, blocks, bd, s); break;
-      case 4: e = launch_stage<4>(st, d_key, is, it, os, ot, c, cs, blocks, bd, s); break;
-      case 8: e = launch_stage<8>(st, d_key, is, it, os, ot, c, cs, blocks, bd, s); break;
-      case 16: e = launch_stage<16>(st, d_key, is, it, os, ot, c, cs, blocks, bd, s); break;
+      case 1: e = PIR_STAGE(1); break;
+      case 2: e = PIR_STAGE(2); break;
+      case 4: e = PIR_STAGE(4); break;
+      case 8: e = PIR_STAGE(8); break;
+      case 16: e = PIR_STAGE(16); break;
       default: return hipErrorInvalidValue;
     }
+#undef PIR_STAGE
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -1104,7 +1105,7 @@ int final_stage_blocks(const TreePlan& pl) {
 
 static int vec_for(int nq) { return nq <= 2 ? 4 : (nq <= 8 ? 2 : 1); }
 
-ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus) {
+ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus, int blocks_per_cu) {
   ScanShape sh{};
   sh.nq = nq;
   sh.nrp = nq == 1 ? 1 : (nq == 2 ? 2 : (nq <= 4 ? 4 : (nq <= 8 ? 8 : 16)));
@@ -1120,7 +1121,7 @@ ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus) {
   const uint32_t rpw = sh.uniform ? 1 : kColGroupLanes / sh.cpr;
   const uint64_t groups = (nrec + rpw - 1) / rpw;
   // 16 waves per CU with 4 x 16 B loads in flight per lane (~64 KiB per CU), few slabs
-  const uint64_t want_blocks = (uint64_t)num_cus * kScanBlocksPerCU;
+  const uint64_t want_blocks = (uint64_t)num_cus * (blocks_per_cu > 0 ? blocks_per_cu : kScanBlocksPerCU);
   const uint64_t waves_per_block = kScanThreads / 64;
   uint64_t gx = std::max<uint64_t>(1, std::min<uint64_t>(want_blocks / gy, (groups + 4 * waves_per_block - 1) / (4 * waves_per_block)));
   sh.grid = dim3((unsigned)gx, gy);

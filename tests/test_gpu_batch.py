@@ -30,6 +30,8 @@ BATCH_SHAPES = [  # (p, n, efs, nq, num_keys, keys per pass; 0 = automatic)
     (2, 12, 256, 1, 13, 0), (2, 10, 96, 1, 8, 16), (2, 11, 1024, 1, 5, 4), (2, 9, 1, 1, 3, 2),
     (3, 11, 100, 3, 5, 0), (3, 10, 48, 2, 9, 8), (5, 9, 48, 4, 7, 4), (8, 10, 64, 5, 3, 2),
     (8, 10, 64, 5, 3, 0), (2, 13, 4096, 1, 4, 8), (17, 8, 40, 16, 2, 0), (9, 9, 32, 1, 17, 16),
+    # more keys than one frontier launch takes (256): frontiers in several launches
+    (2, 6, 16, 1, 300, 0), (3, 7, 24, 2, 270, 4),
 ]
 
 
