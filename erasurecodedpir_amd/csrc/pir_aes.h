@@ -65,6 +65,20 @@ __device__ __forceinline__ void load_tables(uint32_t* lds) {
     lds[i] = (i & 32) ? __builtin_amdgcn_alignbit(v, v, 16) : v;
   }
 }
+// the same for a block of exactly NT threads: every load is issued before the first store,
+// and entry (i >> 6) is wave-uniform, so the loads are scalar
+template <int NT>
+__device__ __forceinline__ void load_tables_n(uint32_t* lds) {
+  constexpr int K = 256 * 64 / NT;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = c_te0[wv + k * (NT / 64)];
+  const bool hi = threadIdx.x & 32;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    lds[threadIdx.x + k * NT] = hi ? __builtin_amdgcn_alignbit(v[k], v[k], 16) : v[k];
+}
 
 // SubWord(RotWord(k3)) ^ rcon, then the word chain (FIPS-197 5.2)
 __device__ __forceinline__ void key_next(const Tab& T, uint32_t& k0, uint32_t& k1, uint32_t& k2,

@@ -90,6 +90,7 @@ struct pir_engine {
   int last_chunks = 1;
   int last_fused = 0;
   bool allow_fused = true;  // $PIR_FUSED=0 forces the 2-kernel path (A/B diagnostics)
+  bool allow_query = true;  // $PIR_QUERY=0: frontier + k_fused instead of k_query
   uint8_t* d_shard = nullptr;
   uint8_t* d_key_raw = nullptr;  // max_batch keys
   pir::DevKey* d_keys = nullptr; // max_batch parsed keys
@@ -232,11 +233,45 @@ int answer_fused(pir_engine* e, const uint8_t* d_raw, int log_parts_total, uint6
   return PIR_OK;
 }
 
+// one launch: key parse, tree and scan in k_query; then the slab reduce
+int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw,
+                 int log_parts_total, uint64_t prefix, uint64_t row0, uint8_t* d_out,
+                 hipStream_t s) {
+  const auto& c = e->cfg;
+  const pir::ScanShape& sh = qp.shape;
+  int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
+  if (rc) return rc;
+  e->last_chunks = 1;
+  e->last_fused = 2;
+  hipEvent_t* ev = e->ev;
+  if (ev) {
+    HIP_TRY(hipEventRecord(ev[EV_KEY], s));
+    HIP_TRY(hipEventRecord(ev[EV_FRONT], s));
+    HIP_TRY(hipEventRecord(ev[EV_LEAF_B], s));
+    HIP_TRY(hipEventRecord(ev[EV_LEAF_E], s));
+    HIP_TRY(hipEventRecord(ev[EV_SCAN_B], s));
+  }
+  HIP_TRY(pir::launch_query(qp, d_raw, c.num_parties, c.log_num_records, c.party_index - 1,
+                            log_parts_total, prefix, e->d_shard + row0 * e->pitch, e->d_slabs, s));
+  if (ev) {
+    HIP_TRY(hipEventRecord(ev[EV_SCAN_E], s));
+    HIP_TRY(hipEventRecord(ev[EV_PRERED], s));
+  }
+  HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, d_out, s));
+  if (ev) HIP_TRY(hipEventRecord(ev[EV_RED], s));
+  return PIR_OK;
+}
+
 int answer_core(pir_engine* e, const uint8_t* d_raw, int log_parts_total, uint64_t prefix,
                 uint64_t row0, uint8_t* d_out, hipStream_t s) {
   const auto& c = e->cfg;
   const pir::DevKey* d_key = e->d_keys;
   const uint64_t nleaves = 1ull << (c.log_num_records - log_parts_total);
+  if (e->allow_query && e->allow_fused) {
+    const pir::QueryPlan qp = pir::make_query_plan(c.log_num_records, log_parts_total,
+                                                   c.num_parties, c.num_rounds, e->pitch, e->num_cus);
+    if (qp.tile) return answer_query(e, qp, d_raw, log_parts_total, prefix, row0, d_out, s);
+  }
   const int tile = e->allow_fused ? pir::fused_tile(c.num_rounds, e->pitch, nleaves, e->num_cus) : 0;
   if (tile) return answer_fused(e, d_raw, log_parts_total, prefix, row0, d_out, s, tile);
   e->last_fused = 0;
@@ -531,6 +566,8 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
   {
     const char* f = getenv("PIR_FUSED");
     e->allow_fused = !(f && f[0] == '0');
+    const char* qy = getenv("PIR_QUERY");
+    e->allow_query = !(qy && qy[0] == '0');
     const char* bg = getenv("PIR_BATCH_G");
     if (bg) e->batch_group = atoi(bg);
     const char* bb = getenv("PIR_BATCH_SCAN_BPC");
@@ -863,6 +900,42 @@ int pir_engine_profile_phases(pir_engine_t* e, const uint8_t* d_key, int iters, 
   }
   for (auto& x : ev) (void)hipEventDestroy(x);
   return PIR_OK;
+}
+
+int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, uint64_t* out, int max_wgs) {
+  if (!e || !d_key || !out || max_wgs < 0) return fail(PIR_EINVAL, "bad argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  const auto& c = e->cfg;
+  HIP_TRY(hipSetDevice(c.device));
+  const pir::QueryPlan qp = pir::make_query_plan(c.log_num_records, c.log_num_partitions,
+                                                 c.num_parties, c.num_rounds, e->pitch, e->num_cus);
+  if (!qp.tile) return fail(PIR_EINVAL, "shape does not use the single-launch query kernel");
+  const pir::ScanShape& sh = qp.shape;
+  int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
+  if (rc) return rc;
+  const int nwg = (int)sh.grid.x;
+  const size_t bytes = (size_t)nwg * pir::kQueryTraceSlots * sizeof(uint64_t);
+  uint64_t* d_tr = nullptr;
+  HIP_TRY(hipMalloc(&d_tr, bytes));
+  std::vector<uint64_t> h((size_t)nwg * pir::kQueryTraceSlots);
+  hipError_t err = hipMemsetAsync(d_tr, 0, bytes, e->stream);
+  if (err == hipSuccess)
+    err = pir::launch_query(qp, d_key, c.num_parties, c.log_num_records, c.party_index - 1,
+                            c.log_num_partitions, (uint64_t)c.partition_index, e->d_shard,
+                            e->d_slabs, e->stream, d_tr);
+  if (err == hipSuccess) err = hipMemcpyAsync(h.data(), d_tr, bytes, hipMemcpyDeviceToHost, e->stream);
+  if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+  (void)hipFree(d_tr);
+  if (err != hipSuccess) return fail(PIR_EHIP, "trace_query: %s", hipGetErrorString(err));
+  uint64_t t0 = ~0ull;
+  for (int w = 0; w < nwg; ++w) t0 = std::min(t0, h[(size_t)w * pir::kQueryTraceSlots]);
+  const int n = std::min(nwg, max_wgs);
+  for (int w = 0; w < n; ++w)
+    for (int k = 0; k < pir::kQueryTraceSlots; ++k) {
+      const uint64_t v = h[(size_t)w * pir::kQueryTraceSlots + k];
+      out[(size_t)w * pir::kQueryTraceSlots + k] = k >= 56 ? v : (v ? v - t0 : 0);
+    }
+  return nwg;
 }
 
 int pir_engine_get_shard(pir_engine_t* e, uint64_t row0, uint64_t nrows, uint8_t* out) {

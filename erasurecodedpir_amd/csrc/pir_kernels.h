@@ -105,6 +105,17 @@ ScanShape make_fused_shape(uint64_t nleaves, uint32_t pitch, int nq, int num_cus
 hipError_t launch_fused(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb,
                         const uint8_t* shard, const ScanShape& sh, uint8_t* slabs, int tile,
                         hipStream_t s);
+// Single-launch query (k_query): key parse + whole tree + scan in one persistent launch of
+// 2^lr workgroups, each owning 2^lt tiles of `tile` leaves.  tile == 0: shape not supported.
+struct QueryPlan {
+  int tile, lr, lt;
+  ScanShape shape;  // grid.x = 2^lr workgroups (slabs), grid.y = column groups
+};
+QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, int num_cus);
+constexpr int kQueryTraceSlots = 64;  // trace: per-workgroup phase stamps (wall clock, 100 MHz)
+hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, int p, int n, int party0,
+                        int log_parts, uint64_t prefix, const uint8_t* shard, uint8_t* slabs,
+                        hipStream_t s, uint64_t* trace = nullptr);
 // XOR the slabs, compact pitch -> record_bytes: d_out[a*efs + b]
 hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t efs,
                          uint8_t* d_out, hipStream_t s);

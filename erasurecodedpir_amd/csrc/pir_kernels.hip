@@ -805,6 +805,413 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// k_query: ONE launch answers one query (no frontier / expand kernels before it).  Workgroup b
+// owns region b of the partition (R = 2^(nr - lr) leaves, nr = n - log_parts) = T tiles of
+// TILE leaves.  Tree waves:
+//   * key: every workgroup parses the correction words of all levels into LDS;
+//   * tile root: wave 0 walks the tree depth-first in column shape (16 lanes per node) from the
+//     root along (prefix, b, tile) -- the first tile descends all Lt = log_parts + lr + log2 T
+//     levels; tile i > 0 pops the right sibling stored when its ancestor was expanded and
+//     descends ctz(i) levels, so the T tile roots cost T - 1 expansions in all;
+//   * tile: expand the root breadth-first in LDS, column shape while a level has <= 32 nodes
+//     (latency), row shape below (throughput), and write the DPF shares into the LDS ring.
+// Scan waves are k_fused's.  The first scan starts after Lt + log2 TILE dependent AES levels.
+// ------------------------------------------------------------------------------------------
+constexpr int kQueryCwCap = 256;  // (levels x (p-1)) correction words staged in LDS
+
+template <int TILE, int NRP, int NQ, int VEC, int GYMAX>
+struct QuerySmem {
+  uint32_t tab[2 * 256 * 32];
+  uint4 sa[TILE / 2];
+  uint32_t ta[TILE / 2];
+  uint4 sb[TILE / 4];
+  uint32_t tb[TILE / 4];
+  uint8_t ring[2][TILE * NRP];
+  uint32_t red[GYMAX][NQ * kColGroupLanes * VEC];
+  uint4 scw[kQueryCwCap];           // sCW[L][j] at L * (p-1) + j
+  uint32_t tcw[kQueryCwCap];
+  uint4 lastcw[kMaxCW];
+  uint4 stk_s[kMaxLevels + 1];      // right siblings on the current root-to-tile path
+  uint32_t stk_t[kMaxLevels + 1];
+  uint32_t bar, ready;
+  uint32_t consumed[2];
+};
+
+__device__ __forceinline__ void cw_lds(const uint4* scw, const uint32_t* tcw, int L, uint32_t t,
+                                       uint32_t pm1, uint4& cs, uint32_t& ct) {
+  cs = make_uint4(0, 0, 0, 0);
+  ct = 0;
+  const int base = L * (int)pm1;
+  for (uint32_t j = 0; j < pm1; ++j) {
+    const uint32_t m = 0u - ((t >> j) & 1u);
+    cs = xor4(cs, and4(scw[base + j], m));
+    ct ^= tcw[base + j] & m;
+  }
+}
+
+template <int NQ, int NRP, int VEC, bool UNI, int TW, int TILE, int GYMAX>
+__global__ __launch_bounds__(kFusedThreads) void k_query(
+    const uint8_t* __restrict__ raw, int p, int n, int nq, int party0, int log_parts,
+    uint64_t prefix, int lr, int lt, const uint8_t* __restrict__ shard, uint32_t pitch,
+    uint32_t cpr, uint32_t gy, uint8_t* __restrict__ slabs, uint64_t* __restrict__ trace) {
+  // trace != nullptr: per-workgroup wall-clock stamps (100 MHz) of the phases, kQueryTraceSlots
+  // apart: start, key parsed, first tile root, tile 0 ready, last tile ready, scan done, end
+  if (trace) trace += (uint64_t)blockIdx.x * kQueryTraceSlots;
+  if (trace && threadIdx.x == 0) { trace[0] = wall_clock64(); trace[56] = clock64(); }
+  constexpr int SW = kFusedWaves - TW;
+  constexpr int CH = VEC * 4;
+  constexpr int GW = kColGroupLanes * VEC;
+  constexpr int NW = NRP <= 4 ? 1 : NRP / 4;
+  constexpr int KT = TILE == 4096 ? 12 : 10;  // log2 TILE
+  using Smem = QuerySmem<TILE, NRP, NQ, VEC, GYMAX>;
+  static_assert(sizeof(Smem) <= 160 * 1024, "LDS");
+  __shared__ Smem sm;
+  const uint32_t pm1 = (uint32_t)p - 1;
+  load_tables_n<kFusedThreads>(sm.tab);
+  for (int i = threadIdx.x; i < GYMAX * NQ * GW; i += blockDim.x) (&sm.red[0][0])[i] = 0;
+  // the key (dpf_tree.cpp:504-519): CWs of every level, lastCW (k_key_prep's layout, in LDS)
+  for (int i = threadIdx.x; i < n * (int)pm1; i += blockDim.x) {
+    const int L = i / (int)pm1, j = i - L * (int)pm1;
+    parse_cw(raw, p, L, j, sm.scw[i], sm.tcw[i]);
+  }
+  for (int j = threadIdx.x; j < kMaxCW; j += blockDim.x) {
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (j < (int)pm1)
+      for (int a = 0; a < nq; ++a)
+        w[a >> 2] |= (uint32_t)raw[16 + n * (int)pm1 * (16 + 2 * p - 2) + a * (int)pm1 + j] << (8 * (a & 3));
+    sm.lastcw[j] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  if (threadIdx.x == 0) { sm.bar = 0; sm.ready = 0; sm.consumed[0] = 0; sm.consumed[1] = 0; }
+  __syncthreads();
+  if (trace && threadIdx.x == 0) trace[1] = wall_clock64();
+
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t b = blockIdx.x;
+  const uint32_t ntiles = 1u << lt;
+  const uint64_t region_rows = (uint64_t)TILE << lt;
+
+  // ======================================= tree work =======================================
+  // tree_tile(i, nt, team): the shares of tile i into ring slot i&1, by the first nt threads
+  // (team = their waves).  Tile 0 is built by all 16 waves (the scan waves have nothing to
+  // read before it); later tiles by the TW tree waves while the scan waves stream.
+  const Tab T(sm.tab);
+  const Bits B((uint32_t)p);
+  const int tt = threadIdx.x;
+  const uint32_t q = tt & 3u, role = (tt >> 2) & 3u;
+  const uint32_t mq1 = q >= 1 ? 0xffffffffu : 0u, mq2 = q >= 2 ? 0xffffffffu : 0u;
+  const uint32_t ptq = q == 3 ? (role << 24) : 0u;  // column shape: CTR block `role`
+  const int Lr = log_parts + lr;  // region root level
+  const int Lt = Lr + lt;         // tile root level
+  const int L_leaf_parent = Lt + KT - 1;
+  uint32_t gen = 0;
+  uint4 qm;
+  {
+    uint32_t m[4];
+    for (int w = 0; w < 4; ++w) {
+      const int nb = nq - 4 * w;
+      m[w] = nb >= 4 ? 0xffffffffu : (nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u));
+    }
+    qm = make_uint4(m[0], m[1], m[2], m[3]);
+  }
+  auto cw = [&](int L, uint32_t tv, uint4& cs, uint32_t& ct) {
+    cw_lds(sm.scw, sm.tcw, L, tv, pm1, cs, ct);
+  };
+  auto tree_tile = [&](uint32_t i, int nt, uint32_t team) {
+    uint8_t* ring = sm.ring[i & 1];
+    // the whole workgroup: hardware barrier (waiting waves sleep); the tree waves alone: LDS
+    // counter barrier (the scan waves keep streaming)
+    auto sync = [&]() {
+      if (team == (uint32_t)kFusedWaves) __syncthreads();
+      else group_barrier(&sm.bar, gen, team);
+    };
+    // ---- tile root (wave 0, column shape, depth-first) ------------------------------------
+    if (wave == 0) {
+      int L0, depth;
+      uint32_t sq, t;
+      uint64_t path;  // bits of the levels still to descend (MSB first)
+      if (i == 0) {
+        L0 = 0;
+        depth = Lt;
+        sq = load_le32(raw + 4 * q);
+        t = party0 >= 1 ? (1u << (party0 - 1)) : 0u;  // dpf_tree.cpp:496-502
+        path = (((prefix << lr) | b) << lt);
+      } else {
+        const int j = __builtin_ctz(i);
+        L0 = Lt - j;  // the right sibling popped at level L0, then j left turns
+        depth = j;
+        sq = reinterpret_cast<const uint32_t*>(&sm.stk_s[L0])[q];
+        t = sm.stk_t[L0];
+        path = 0;
+      }
+      // the 4 groups of 16 lanes compute the same node; the path bit is wave-uniform, so the
+      // chosen child moves to every lane through SGPRs (v_readlane), not through the LDS
+      const uint32_t m0 = q == 0 ? ~0u : 0u, m1 = q == 1 ? ~0u : 0u;
+      const uint32_t m2 = q == 2 ? ~0u : 0u, m3 = q == 3 ? ~0u : 0u;
+      for (int d = 0; d < depth; ++d) {
+        const int L = L0 + d;
+        // word q of the correction word (t is wave-uniform here); issued before the rounds
+        uint32_t csq = 0, ct = 0;
+        for (uint32_t j = 0; j < pm1; ++j) {
+          const uint32_t m = 0u - ((t >> j) & 1u);
+          csq ^= reinterpret_cast<const uint32_t*>(&sm.scw[L * (int)pm1 + (int)j])[q] & m;
+          ct ^= sm.tcw[L * (int)pm1 + (int)j] & m;
+        }
+        const uint32_t o = aes_col(T, sq, ptq, mq1, mq2);
+        const uint32_t bit = (uint32_t)((path >> (depth - 1 - d)) & 1u);
+        const uint32_t oc = o ^ csq;
+        const uint32_t tbits = (__builtin_amdgcn_readlane(o, 8) & B.tb_mask) ^
+                               __builtin_amdgcn_readfirstlane(ct);
+        if (L >= Lr && bit == 0) {  // inside the region: keep the right child for later tiles
+          if (lane >= 4 && lane < 8) reinterpret_cast<uint32_t*>(&sm.stk_s[L + 1])[lane - 4] = oc;
+          if (lane == 0) sm.stk_t[L + 1] = (tbits >> pm1) & B.tmask;
+        }
+        const uint32_t c0 = __builtin_amdgcn_readlane(oc, (int)(4 * bit + 0));
+        const uint32_t c1 = __builtin_amdgcn_readlane(oc, (int)(4 * bit + 1));
+        const uint32_t c2 = __builtin_amdgcn_readlane(oc, (int)(4 * bit + 2));
+        const uint32_t c3 = __builtin_amdgcn_readlane(oc, (int)(4 * bit + 3));
+        sq = (c0 & m0) | (c1 & m1) | (c2 & m2) | (c3 & m3);
+        t = (tbits >> (bit * pm1)) & B.tmask;
+        if (trace && i == 0 && lane == 0 && d < 32) trace[8 + d] = wall_clock64();
+      }
+      uint4* s0 = ((KT - 1) & 1) ? sm.sb : sm.sa;
+      uint32_t* t0 = ((KT - 1) & 1) ? sm.tb : sm.ta;
+      if (lane < 4) reinterpret_cast<uint32_t*>(&s0[0])[lane] = sq;
+      if (lane == 0) t0[0] = t;
+      if (trace && i == 0 && lane == 0) { trace[2] = wall_clock64(); trace[57] = clock64(); }
+    }
+    sync();
+    // ---- breadth-first expansion of the tile root ------------------------------------------
+    // level i of a tile (width 2^i) lives in buffer a when (KT-1-i) is even, else b
+    int buf = (KT - 1) & 1;
+    int W = 1;
+    for (int lv = 0; lv < KT - 1; ++lv) {
+      const int L = Lt + lv;
+      const uint4* is = buf ? sm.sb : sm.sa;
+      const uint32_t* it = buf ? sm.tb : sm.ta;
+      uint4* os = buf ? sm.sa : sm.sb;
+      uint32_t* ot = buf ? sm.ta : sm.tb;
+      if (W * 16 <= nt) {  // column shape: 16 lanes per node
+        const int u = tt >> 4;
+        if (u < W) {  // uniform per 16-lane group
+          const uint32_t s_in = reinterpret_cast<const uint32_t*>(&is[u])[q], t_in = it[u];
+          uint4 cs;
+          uint32_t ct;
+          cw(L, t_in, cs, ct);
+          const uint32_t o = aes_col(T, s_in, ptq, mq1, mq2);
+          if (role < 2) {
+            reinterpret_cast<uint32_t*>(&os[2 * u + role])[q] = o ^ word_of(cs, q);
+          } else if (role == 2 && q == 0) {
+            const uint32_t tb = (o & B.tb_mask) ^ ct;
+            ot[2 * u] = tb & B.tmask;
+            ot[2 * u + 1] = (tb >> B.pm1) & B.tmask;
+          }
+        }
+      } else if (team == (uint32_t)kFusedWaves) {
+        // 3 lanes per node, lane r runs CTR block r with its own key schedule: a third of the
+        // row-shape latency when the whole workgroup expands a narrow-ish level (tile 0)
+        const int l = tt & 63, ul = l / 3, r = l - 3 * ul;
+        const int npp = (nt >> 6) * 21;
+        for (int u = (tt >> 6) * 21 + ul; l < 63 && u < W; u += npp) {
+          uint4 cs;
+          uint32_t ct;
+          cw(L, it[u], cs, ct);
+          const uint4 o = aes_ctr_block(T, is[u], (uint32_t)r);
+          if (r < 2) {
+            os[2 * u + r] = xor4(o, cs);
+          } else {
+            const uint32_t tb = (o.x & B.tb_mask) ^ ct;
+            ot[2 * u] = tb & B.tmask;
+            ot[2 * u + 1] = (tb >> B.pm1) & B.tmask;
+          }
+        }
+      } else {  // row shape: one lane per node, 3 CTR blocks on one key schedule
+        for (int u = tt; u < W; u += nt) {
+          uint4 cs;
+          uint32_t ct;
+          cw(L, it[u], cs, ct);
+          uint4 o[3];
+          aes_ctr_row<3, 1>(T, is[u], o);
+          const uint32_t tb = (o[2].x & B.tb_mask) ^ ct;
+          os[2 * u] = xor4(o[0], cs);
+          os[2 * u + 1] = xor4(o[1], cs);
+          ot[2 * u] = tb & B.tmask;
+          ot[2 * u + 1] = (tb >> B.pm1) & B.tmask;
+        }
+      }
+      sync();
+      if (trace && i == 0 && tt == 0 && lv < 16) trace[40 + lv] = wall_clock64();
+      buf ^= 1;
+      W *= 2;
+    }
+    if (team == (uint32_t)kFusedWaves) {  // last level + leaves, 3 lanes per parent
+      const uint4* is = buf ? sm.sb : sm.sa;
+      const uint32_t* it = buf ? sm.tb : sm.ta;
+      const int l = tt & 63, ul = l / 3, r = l - 3 * ul;
+      const int npp = (nt >> 6) * 21;
+      const int u0 = (tt >> 6) * 21 + ul;
+      const int src = (l < 63 ? l - r + 2 : l);  // the node's control-bit lane
+      for (int ub = 0; ub < W; ub += npp) {  // uniform trip count: every lane joins the shuffle
+        const int u = u0 + ub;
+        const bool act = l < 63 && u < W;
+        uint4 cs = make_uint4(0, 0, 0, 0);
+        uint32_t ct = 0;
+        uint4 o = make_uint4(0, 0, 0, 0);
+        if (act) {
+          cw(L_leaf_parent, it[u], cs, ct);
+          o = aes_ctr_block(T, is[u], (uint32_t)r);
+        }
+        const uint32_t tb = (uint32_t)__shfl((int)((o.x & B.tb_mask) ^ ct), src, 64);
+        if (act && r < 2) {
+          const uint32_t tc = (tb >> (r * pm1)) & B.tmask;
+          uint4 v = aes_ctr_block(T, xor4(o, cs), 0u);
+          for (uint32_t j = 0; j < pm1; ++j) v = xor4(v, and4(sm.lastcw[j], 0u - ((tc >> j) & 1u)));
+          store_leaf<NRP>(ring, 2 * u + r, make_uint4(v.x & qm.x, v.y & qm.y, v.z & qm.z, v.w & qm.w));
+        }
+      }
+    } else {  // last level + leaf conversion (dpf_tree.cpp:567-580) into the ring
+      const uint4* is = buf ? sm.sb : sm.sa;
+      const uint32_t* it = buf ? sm.tb : sm.ta;
+      for (int u = tt; u < W; u += nt) {
+        uint4 cs;
+        uint32_t ct;
+        cw(L_leaf_parent, it[u], cs, ct);
+        uint4 o[3];
+        aes_ctr_row<3, 1>(T, is[u], o);
+        const uint32_t tb = (o[2].x & B.tb_mask) ^ ct;
+        const uint32_t tl = tb & B.tmask, tr = (tb >> B.pm1) & B.tmask;
+        uint4 vl[1], vr[1];
+        aes_ctr_row<1, NW>(T, xor4(o[0], cs), vl);
+        aes_ctr_row<1, NW>(T, xor4(o[1], cs), vr);
+        for (uint32_t j = 0; j < pm1; ++j) {
+          vl[0] = xor4(vl[0], and4(sm.lastcw[j], 0u - ((tl >> j) & 1u)));
+          vr[0] = xor4(vr[0], and4(sm.lastcw[j], 0u - ((tr >> j) & 1u)));
+        }
+        const uint4 a = make_uint4(vl[0].x & qm.x, vl[0].y & qm.y, vl[0].z & qm.z, vl[0].w & qm.w);
+        const uint4 c = make_uint4(vr[0].x & qm.x, vr[0].y & qm.y, vr[0].z & qm.z, vr[0].w & qm.w);
+        if constexpr (NRP == 1) {
+          *reinterpret_cast<uint16_t*>(ring + 2 * u) = (uint16_t)((a.x & 0xffu) | ((c.x & 0xffu) << 8));
+        } else {
+          store_leaf<NRP>(ring, 2 * u, a);
+          store_leaf<NRP>(ring, 2 * u + 1, c);
+        }
+      }
+    }
+    sync();  // every share of tile i is in the ring
+    if (wave == 0) lds_signal(&sm.ready);
+    if (trace && tt == 0 && (i == 0 || i == ntiles - 1)) trace[i == 0 ? 3 : 4] = wall_clock64();
+  };
+
+  tree_tile(0, kFusedThreads, kFusedWaves);  // every wave builds the first tile
+  if (wave < (uint32_t)TW) {
+    // ===================================== tree role ======================================
+    for (uint32_t i = 1; i < ntiles; ++i) {
+      if (i >= 2) lds_wait_geq(&sm.consumed[i & 1], (i >> 1) * SW);
+      tree_tile(i, TW * 64, TW);
+    }
+  } else {
+    // ===================================== scan role ======================================
+    const uint32_t sw = wave - TW;
+    uint32_t gcol, wi, nwg, rpw, rec_off, chunk;
+    bool active;
+    if (UNI) {
+      gcol = sw % gy;
+      wi = sw / gy;
+      nwg = SW / gy;
+      rpw = 1; rec_off = 0;
+      chunk = gcol * kColGroupLanes + lane;
+      active = chunk < cpr && wi < nwg;
+    } else {
+      gcol = 0; wi = sw; nwg = SW;
+      rpw = kColGroupLanes / cpr;
+      rec_off = lane / cpr;
+      chunk = lane - rec_off * cpr;
+      active = lane < rpw * cpr;
+    }
+    uint32_t Z[NQ][8][VEC];
+#pragma unroll
+    for (int a = 0; a < NQ; ++a)
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) Z[a][kk][v] = 0;
+    const uint32_t ngroups = (TILE + rpw - 1) / rpw;
+    constexpr int U = SW >= 8 ? 8 : 16;
+    __builtin_amdgcn_s_setprio(2);
+    const uint8_t* rbase = shard + (b * region_rows) * pitch + (uint64_t)chunk * CH;
+    for (uint32_t i = 0; i < ntiles; ++i) {
+      const uint8_t* ring = sm.ring[i & 1];
+      lds_wait_geq(&sm.ready, i + 1);
+      if (wi < nwg) {
+        const uint8_t* base = rbase + ((uint64_t)i * TILE) * pitch;
+        for (uint32_t g0 = wi; g0 < ngroups; g0 += U * nwg) {
+          Chunk<VEC> x[U];
+          uint4 cf[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t gi = g0 + u * nwg;
+            const uint32_t rl = gi * rpw + rec_off;
+            const bool ok = active && gi < ngroups && rl < TILE;
+            if (ok) x[u] = load_chunk<VEC>(base + (uint64_t)rl * pitch);
+            else
+              for (int v = 0; v < VEC; ++v) x[u].v[v] = 0;
+            if (UNI) {
+              const uint32_t gu = __builtin_amdgcn_readfirstlane(gi);
+              uint4 c4 = gu < ngroups ? load_coef<NRP>(ring, gu) : make_uint4(0, 0, 0, 0);
+              cf[u] = make_uint4(__builtin_amdgcn_readfirstlane(c4.x), __builtin_amdgcn_readfirstlane(c4.y),
+                                 __builtin_amdgcn_readfirstlane(c4.z), __builtin_amdgcn_readfirstlane(c4.w));
+            } else {
+              cf[u] = ok ? load_coef<NRP>(ring, rl) : make_uint4(0, 0, 0, 0);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int a = 0; a < NQ; ++a) {
+              const uint32_t ca = coef_byte(cf[u], a);
+              if (UNI) {
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk)
+                  if (ca & (1u << kk)) {
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= x[u].v[v];
+                  }
+              } else {
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk) {
+                  const uint32_t m = 0u - ((ca >> kk) & 1u);
+#pragma unroll
+                  for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= x[u].v[v] & m;
+                }
+              }
+            }
+        }
+      }
+      lds_signal(&sm.consumed[i & 1]);
+    }
+    if (trace && sw == 0 && lane == 0) trace[5] = wall_clock64();
+    if (active) {
+      const uint32_t wbase = (UNI ? lane : chunk) * VEC;
+#pragma unroll
+      for (int a = 0; a < NQ; ++a)
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          uint32_t acc = Z[a][7][v];
+#pragma unroll
+          for (int kk = 6; kk >= 0; --kk) acc = gf_xtime4(acc) ^ Z[a][kk][v];
+          if (acc) atomicXor(&sm.red[gcol][a * GW + wbase + v], acc);
+        }
+    }
+  }
+  __syncthreads();
+  for (uint32_t g = 0; g < gy; ++g) {
+    uint32_t* slab = reinterpret_cast<uint32_t*>(slabs) + ((uint64_t)g * gridDim.x + blockIdx.x) * (NQ * GW);
+    for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) slab[i] = sm.red[g][i];
+  }
+  if (trace && threadIdx.x == 0) trace[6] = wall_clock64();
+}
+
 // slabs: [grid.y][grid.x][nq][GW words]; out[a*efs + b] for b < efs.
 // One 1024-thread block per 64 output words: 16 lane groups split the gx slabs, then LDS.
 __global__ __launch_bounds__(kReduceThreads) void k_reduce(const uint32_t* __restrict__ slabs,
@@ -1016,6 +1423,71 @@ hipError_t launch_fused(const TreePlan& pl, const DevKey* d_key, const NodeBufs&
 }
 
 int fused_k(int tile) { return tile == 4096 ? 6 : (tile == 1024 ? 4 : 0); }
+
+// ---- single-launch query ---------------------------------------------------------------------
+QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, int num_cus) {
+  QueryPlan qp{};
+  const int nr = n - log_parts;
+  if (nr < 0 || (uint64_t)n * (uint64_t)(p - 1) > (uint64_t)kQueryCwCap) return qp;
+  const uint64_t nleaves = 1ull << nr;
+  const int tile = fused_tile(nq, pitch, nleaves, num_cus);
+  if (!tile) return qp;
+  const int kt = tile == 4096 ? 12 : 10;
+  int lr = 0;
+  while ((2ll << lr) <= num_cus) ++lr;  // regions = largest power of two <= CUs
+  lr = std::min(lr, nr - kt);
+  if (lr < 0) return qp;
+  qp.tile = tile;
+  qp.lr = lr;
+  qp.lt = nr - kt - lr;
+  qp.shape = make_fused_shape(nleaves, pitch, nq, num_cus, tile);
+  qp.shape.grid.x = 1u << lr;
+  return qp;
+}
+
+template <int NQ, int TILE>
+static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, int p, int n, int party0,
+                           int log_parts, uint64_t prefix, const uint8_t* shard, uint8_t* slabs,
+                           hipStream_t s, uint64_t* trace) {
+  constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : 8));
+  constexpr int VEC = NQ <= 2 ? 4 : 2;
+  const ScanShape& sh = qp.shape;
+  if (sh.uniform)
+    hipLaunchKernelGGL((k_query<NQ, NRP, VEC, true, kFusedTW, TILE, 4>), dim3(sh.grid.x),
+                       dim3(kFusedThreads), 0, s, d_raw, p, n, NQ, party0, log_parts, prefix,
+                       qp.lr, qp.lt, shard, sh.pitch, sh.cpr, sh.grid.y, slabs, trace);
+  else
+    hipLaunchKernelGGL((k_query<NQ, NRP, VEC, false, kFusedTW, TILE, 1>), dim3(sh.grid.x),
+                       dim3(kFusedThreads), 0, s, d_raw, p, n, NQ, party0, log_parts, prefix,
+                       qp.lr, qp.lt, shard, sh.pitch, sh.cpr, 1u, slabs, trace);
+  return hipGetLastError();
+}
+
+hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, int p, int n, int party0,
+                        int log_parts, uint64_t prefix, const uint8_t* shard, uint8_t* slabs,
+                        hipStream_t s, uint64_t* trace) {
+#define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, p, n, party0, log_parts, prefix, shard, slabs, s, trace)
+  if (qp.tile == 4096) {
+    switch (qp.shape.nq) {
+      case 1: return PIR_Q(1, 4096);
+      case 2: return PIR_Q(2, 4096);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if (qp.tile != 1024) return hipErrorInvalidValue;
+  switch (qp.shape.nq) {
+    case 1: return PIR_Q(1, 1024);
+    case 2: return PIR_Q(2, 1024);
+    case 3: return PIR_Q(3, 1024);
+    case 4: return PIR_Q(4, 1024);
+    case 5: return PIR_Q(5, 1024);
+    case 6: return PIR_Q(6, 1024);
+    case 7: return PIR_Q(7, 1024);
+    case 8: return PIR_Q(8, 1024);
+    default: return hipErrorInvalidValue;
+  }
+#undef PIR_Q
+}
 
 hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys, int p, int n,
                            int nq, int party0, DevKey* d_keys, hipStream_t s) {

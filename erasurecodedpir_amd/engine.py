@@ -197,6 +197,18 @@ class Engine:
         names = ["key_prep", "tree_frontier", "tree_stages", "scan", "reduce"]
         return {n: float(out[i]) for i, n in enumerate(names)}
 
+    TRACE_PHASES = ["start", "key_parsed", "first_tile_root", "tile0_ready", "last_tile_ready",
+                    "scan_done", "end"]
+
+    def trace_query(self, d_key):
+        """One single-launch answer with per-workgroup phase stamps (diagnostics): an array
+        [workgroups, 64] of microseconds since the earliest workgroup start (layout:
+        pir_engine_trace_query in include/pir_engine.h; 0 = stamp not reached)."""
+        out = np.zeros((4096, 64), np.uint64)
+        n = self._lib.pir_engine_trace_query(self._h, d_key, out.ctypes.data_as(ctypes.c_void_p), 4096)
+        check(min(n, 0), "trace_query")
+        return out[:n].astype(np.float64) / 100.0
+
     # -- split shard ---------------------------------------------------------------------------
     def attach_comm(self, unique_id, nranks, rank):
         uid, up = _buf(unique_id)

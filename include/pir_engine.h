@@ -119,6 +119,13 @@ int pir_engine_last_timings(pir_engine_t *e, pir_kernel_time *out, int max);
  * mean ms of key_prep, tree_frontier, tree_stages (all expand stages), scan (one launch over
  * all rows), reduce.  d_key: device pointer to one raw key. */
 int pir_engine_profile_phases(pir_engine_t *e, const uint8_t *d_key, int iters, float *out_ms);
+/* diagnostics: one single-launch answer (k_query) with per-workgroup phase stamps.  out holds
+ * max_wgs x 64 uint64 wall-clock ticks (100 MHz) relative to the earliest start (0 = not
+ * reached): [0..6] start, key parsed, first tile root, tile 0 shares ready, last tile ready,
+ * scan done, end; [8+d] descent level d of the first tile root (d < 32); [40+l] expansion level
+ * l of tile 0 (l < 16).  Returns the number of workgroups (>= 0), or an error code;
+ * PIR_EINVAL when the shape does not use k_query. */
+int pir_engine_trace_query(pir_engine_t *e, const uint8_t *d_key, uint64_t *out, int max_wgs);
 
 /* ---- split shard across GPUs: XOR all-reduce of partition answers over RCCL ---- */
 #define PIR_COMM_ID_BYTES 128

@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Phase timeline of one single-launch answer (k_query), from per-workgroup wall-clock stamps.
+
+    python tools/trace_query.py [--n 20] [--efs 1024] [--p 2] [--nq 1]
+
+Prints, for each phase stamp, min / median / max over workgroups in microseconds since the
+earliest workgroup start (diagnostics; not part of the product path)."""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=20)
+    ap.add_argument("--efs", type=int, default=1024)
+    ap.add_argument("--p", type=int, default=2)
+    ap.add_argument("--nq", type=int, default=1)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    import erasurecodedpir_amd as pir
+    e = pir.Engine(a.p, 1, a.n, a.efs, a.nq)
+    e.fill_shard_random(1)
+    keys = pir.gen_keys(a.n, (1 << a.n) // 3, a.p, a.nq)
+    d_key = e.alloc_dev(e.key_len)
+    e.h2d(d_key, keys[0])
+    for _ in range(3):
+        e.answer(keys[0])
+    for r in range(a.reps):
+        tr = e.trace_query(d_key)
+        print(f"n={a.n} efs={a.efs} p={a.p} nq={a.nq}: {tr.shape[0]} workgroups (rep {r})")
+        for i, name in enumerate(e.TRACE_PHASES):
+            col = tr[:, i]
+            print(f"  {name:16s} min {col.min():8.2f}  med {np.median(col):8.2f}  max {col.max():8.2f} us")
+        med = np.median(tr, axis=0)
+        desc = [med[8 + d] for d in range(32) if tr[:, 8 + d].all()]
+        lev = [med[40 + k] for k in range(16) if tr[:, 40 + k].all()]
+        print("  descent level ends (med us):", " ".join(f"{v:.1f}" for v in desc))
+        print("  tile-0 level ends  (med us):", " ".join(f"{v:.1f}" for v in lev))
+        raw = tr * 100.0  # back to ticks for the clock columns
+        ghz = (raw[:, 57] - raw[:, 56]) / ((tr[:, 2] - tr[:, 0]) * 1e3)
+        print(f"  shader clock start->first root: med {np.median(ghz):.3f} GHz (min {ghz.min():.3f} max {ghz.max():.3f})")
+    e.close()
+
+
+if __name__ == "__main__":
+    main()
