@@ -6,7 +6,11 @@
 A step = one PIR query answered against the device-resident shard: key parse -> DPF
 full-domain evaluation (AES-128 PRG tree) -> GF(2^8) inner product over every record ->
 partial-answer reduce (-> RCCL all-gather + XOR fold across GPUs when N > 1).  Inputs (shard,
-key) are resident in HBM before the timed region; the answer stays in HBM.
+keys) are resident in HBM before the timed region; the answers stay in HBM.  The K timed steps
+are K independent queries (distinct keys) answered as a queue: one launch of the query kernel,
+each query still its own tree and its own full shard pass, the tree of query k+1 built while
+query k's rows stream.  The same K queries answered one launch at a time are reported as
+`single_query` (the per-query latency).
 
 N = 1: BASELINE configs[1] ("c2"): one shard of 2^20 x 1 KiB, DPF depth 20, batch = 1 query.
 N > 1: the split-shard layout (configs[3]'s structure), weak scaling: every GPU holds a 2^20 x
@@ -15,8 +19,8 @@ its partition and the partial answers are XOR-all-reduced over RCCL.  `value` = 
 bytes / time per query (whole job).  Launched per the driver contract with
 torch.distributed.run (gloo carries the barrier / timing max / RCCL unique id).
 
-rank 0 also prints the roofline of the dominant kernel (the GF scan: algorithmic bytes =
-records x record_bytes per launch, HIP-event duration measured inside the timed region) and a
+rank 0 also prints the roofline of the dominant kernel (k_query: algorithmic bytes = K x
+records x record_bytes per launch, HIP-event duration of the launch) and a
 CPU baseline: the reference src/c (oracle/_ref/libref.so, compiled from the reference's own
 sources) -- or the oracle restatement if that is absent -- timed on this host on a bounded
 sample of the same workload; the CPU answer is also checked against the GPU answer bit-exactly.
@@ -114,6 +118,9 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + sorted(BATCH_CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--queue-only", action="store_true",
+                    help="profiling passes: only the warm-up and timed queues (every launch of "
+                         "the query kernel then answers the same number of queries)")
     args = ap.parse_args()
 
     world, rank, local = dist_env()
@@ -141,13 +148,23 @@ def main():
     if world > 1:
         uid = broadcast_bytes(pir.comm_unique_id() if rank == 0 else None)
         eng.attach_comm(uid, world, rank)
-    idx = (1 << n) // 3 + 7
-    seeds = broadcast_bytes(os.urandom(16 * p) if rank == 0 else None) if world > 1 else os.urandom(16 * p)
+    # K + W independent queries (distinct indices, fresh root seeds); every rank holds the same keys
+    nkeys = args.steps + max(args.warmup, 1)
+    seed = int.from_bytes(broadcast_bytes(os.urandom(8) if rank == 0 else None)
+                          if world > 1 else os.urandom(8), "little")
+    rng = np.random.default_rng(seed)
+    idxs = [int(i) for i in rng.choice(1 << n, nkeys, replace=False)]
+    idxs[0] = (1 << n) // 3 + 7
     fcw = pir.final_cw(p, nq, 1)
-    keys = pir.gen_keys(n, idx, p, nq, fcw=fcw, seeds=seeds, device=local)
-    d_key = eng.alloc_dev(eng.key_len)
-    d_res = eng.alloc_dev(eng.answer_bytes)
-    eng.h2d(d_key, keys[0])
+    keys = [pir.gen_keys(n, i, p, nq, fcw=fcw,
+                         seeds=rng.integers(0, 256, 16 * p, dtype=np.uint8).tobytes(), device=local)
+            for i in idxs]
+    kl, ab = eng.key_len, eng.answer_bytes
+    d_keys = eng.alloc_dev(kl * nkeys)
+    d_res = eng.alloc_dev(ab * nkeys)
+    eng.h2d(d_keys, b"".join(k[0] for k in keys))
+    W, K = max(args.warmup, 1), args.steps
+    d_kq, d_rq = d_keys + W * kl, d_res + W * ab  # the timed queue: keys W .. W+K-1
 
     def barrier_sync():
         eng.sync()
@@ -155,11 +172,10 @@ def main():
         if world > 1:
             dist.barrier()
 
-    def timed(steps):
+    def timed(fn):
         barrier_sync()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            eng.answer_dev(d_key, d_res)
+        fn()
         barrier_sync()
         dt = time.perf_counter() - t0
         if world > 1:
@@ -168,26 +184,46 @@ def main():
             dt = float(tt.item())
         return dt
 
-    for _ in range(args.warmup):
-        eng.answer_dev(d_key, d_res)
-    # (1) the measurement: K un-instrumented steps
-    dt = timed(args.steps)
-    ms = dt / args.steps * 1e3
-    # (2) the same K steps with HIP events around every kernel (per-phase device time, the
-    #     scan kernel's duration for the roofline); reported, never used for `value`
-    eng.set_profiling(max(args.steps, 1))
-    dt_prof = timed(args.steps)
-    phases = eng.last_timings()
+    # (1) the measurement: a queue of K independent queries (each its own DPF tree and its own
+    #     full pass over the shard), answered back to back in one launch after W warm-up queries
+    eng.answer_stream_dev(d_keys, W, d_res)
+    dt = timed(lambda: eng.answer_stream_dev(d_kq, K, d_rq))
+    ms = dt / K * 1e3
+    if args.queue_only:
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": round(float(1 << n) * efs / GIB / (ms / 1e3), 3),
+                              "unit": "GiB/s", "ms_per_step": round(ms, 5), "steps": K,
+                              "warmup": W, "mode": "queue-only profiling pass"}), flush=True)
+        eng.close()
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    # (2) the same queue with HIP events around the launch: the query kernel's duration (for
+    #     the roofline) and the phases; reported, never used for `value`
+    eng.set_profiling(1)
+    eng.answer_stream_dev(d_kq, K, d_rq)
+    phases_q = eng.last_timings()
     eng.set_profiling(0)
-    alone = eng.profile_phases(d_key, 10)
-    gpu_answer = eng.d2h(d_res, eng.answer_bytes).reshape(nq, efs)
+    queue_answers = eng.d2h(d_rq, ab * K).reshape(K, nq, efs)
+    # (3) one query at a time (answer_dev per step): single-query latency
+    dt1 = timed(lambda: [eng.answer_dev(d_kq + i * kl, d_rq + i * ab) for i in range(K)])
+    ms1 = dt1 / K * 1e3
+    single_answers = eng.d2h(d_rq, ab * K).reshape(K, nq, efs)
+    eng.set_profiling(max(K, 1))
+    for i in range(K):
+        eng.answer_dev(d_kq + i * kl, d_rq + i * ab)
+    phases1 = eng.last_timings()
+    eng.set_profiling(0)
+    alone = eng.profile_phases(d_keys, 10)
 
     # PIR correctness at full size (every rank): party-1 ^ party-2 answers == finalCW * record
     # (p=2) -- checked with the host API, which also gives the PCIe-inclusive rate.
-    incl_steps = min(20, args.steps)
+    k0 = keys[W][0]
+    incl_steps = min(20, K)
     t1 = time.perf_counter()
     for _ in range(incl_steps):
-        a1 = eng.answer(keys[0])
+        a1 = eng.answer(k0)
     incl_ms = (time.perf_counter() - t1) / incl_steps * 1e3
     pir_ok = None
     if p == 2 and nq == 1:
@@ -197,29 +233,32 @@ def main():
         if world > 1:
             uid2 = broadcast_bytes(pir.comm_unique_id() if rank == 0 else None)
             eng2.attach_comm(uid2, world, rank)
-        a2 = eng2.answer(keys[1])
+        a2 = eng2.answer(keys[W][1])
         eng2.close()
+        idx = idxs[W]
         owner = idx >> (n - g) if g else 0
         rec = eng.shard_row(idx - owner * eng.num_rows) if rank == owner else None
         if world > 1:
             rec = broadcast_from(rec, owner, efs)
         tab = _gf_table(int(fcw[0]))
         pir_ok = bool(np.array_equal(a1[0] ^ a2[0], tab[rec]))
-    same = bool(np.array_equal(a1, gpu_answer))
+    same = bool(np.array_equal(a1, single_answers[0]))
+    queue_same = bool(np.array_equal(queue_answers, single_answers))
 
     shard_bytes = float(1 << n) * efs  # logical shard (all ranks)
     value = shard_bytes / GIB / (ms / 1e3)
-    scan_ms = phases.get("scan", float("nan"))  # summed over the pipelined chunks
-    chunks = int(round(phases.get("chunks", 1))) or 1
+    kern_ms = phases_q.get("scan", float("nan"))  # the k_query launch (all K queries)
     local_bytes = float(eng.num_rows) * efs
-    achieved = local_bytes / (scan_ms / 1e3) / 1e9 if scan_ms == scan_ms and scan_ms > 0 else None
+    algo = local_bytes * K
+    achieved = algo / (kern_ms / 1e3) / 1e9 if kern_ms == kern_ms and kern_ms > 0 else None
+    path = {2.0: "k_query", 1.0: "k_fused", 0.0: "k_expand+k_scan"}.get(phases_q.get("fused"), "?")
     out = {
         "metric": METRIC,
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
+        "steps": K,
+        "warmup": W,
         "ms_per_step": round(ms, 5),
         "higher_is_better": True,
         "scaling": "weak",
@@ -231,30 +270,39 @@ def main():
             "records": 1 << n, "record_bytes": efs, "parties": p, "num_rounds": nq,
             "records_per_gpu": int(eng.num_rows), "dpf_depth": n,
             "parallelism": "split-shard" if world > 1 else "single",
+            "step": "one PIR query: its own DPF key and tree, one full pass over the shard",
+            "mode": "query queue: the K timed queries (distinct keys) are answered back to back "
+                    "in one launch, the tree of query k+1 built while query k streams",
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_scan (GF(2^8) shard scan)",
+            "kernel": f"{path} (DPF tree + GF(2^8) shard scan, {K} queries per launch)",
             "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": _pmc_traffic(args.config, world),
-            "algorithmic_bytes_per_launch": int(local_bytes / chunks),
-            "launches_per_step": chunks,
-            "scan_ms_per_launch": round(scan_ms / chunks, 5),
+            "traffic": _pmc_traffic(args.config, world, K),
+            "algorithmic_bytes_per_launch": int(algo),
+            "algorithmic_bytes_per_query": int(local_bytes),
+            "kernel_ms_per_launch": round(kern_ms, 5),
         },
-        "phases_ms": {k: round(v, 5) for k, v in phases.items() if k != "chunks"},
+        "single_query": {
+            "ms_per_query": round(ms1, 5),
+            "value": round(shard_bytes / GIB / (ms1 / 1e3), 3),
+            "unit": "GiB/s",
+            "note": "answer_dev per step (one launch per query, nothing queued behind it)",
+            "phases_ms": {k: round(v, 5) for k, v in phases1.items() if k != "chunks"},
+        },
         "phases_alone_ms": {k: round(v, 5) for k, v in alone.items()},
-        "instrumented_ms_per_step": round(dt_prof / args.steps * 1e3, 5),
         "inclusive_h2d_key_d2h_answer": {"ms_per_query": round(incl_ms, 4),
                                          "value": round(shard_bytes / GIB / (incl_ms / 1e3), 3),
                                          "unit": "GiB/s"},
-        "parity": {"pir_record_recovered": pir_ok, "host_api_equals_device_api": same},
+        "parity": {"pir_record_recovered": pir_ok, "host_api_equals_device_api": same,
+                   "queue_equals_one_at_a_time": queue_same},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         shard_rows = eng.get_shard()
-        out["cpu_baseline"] = cpu_baseline(keys[0], shard_rows, n, efs, p, nq, gpu_answer,
+        out["cpu_baseline"] = cpu_baseline(k0, shard_rows, n, efs, p, nq, single_answers[0],
                                            args.cpu_budget)
         out["parity"]["gpu_equals_cpu_reference"] = out["cpu_baseline"]["bit_exact_vs_gpu"]
         del shard_rows
@@ -379,13 +427,15 @@ def _gf_table(c):
     return t
 
 
-def _pmc_traffic(config, world):
-    """HBM bytes per scan launch from the committed rocprofv3 --pmc pass (profiles/), if any."""
-    path = os.path.join(ROOT, "profiles", f"pmc_scan_{config}.json")
+def _pmc_traffic(config, world, queries_per_launch):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc passes
+    (profiles/pmc_<config>.json: bytes per query, measured), scaled to the launch's queries."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if world != 1 or not os.path.exists(path):
         return None
     try:
-        return json.load(open(path)).get("hbm_bytes_per_launch")
+        per_q = json.load(open(path)).get("hbm_bytes_per_query")
+        return int(per_q * queries_per_launch) if per_q else None
     except (OSError, ValueError):
         return None
 

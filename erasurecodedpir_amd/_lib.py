@@ -76,6 +76,7 @@ PROTOTYPES = {
     "pir_engine_answer_dev": (_I, [_P, _P, _P, _P]),
     "pir_engine_answer_batch_dev": (_I, [_P, _P, _I, _P, _P]),
     "pir_engine_answer_batch": (_I, [_P, _P, _I, _P]),
+    "pir_engine_answer_stream_dev": (_I, [_P, _P, _I, _P, _P]),
     "pir_engine_set_batch_group": (_I, [_P, _I]),
     "pir_engine_batch_group": (_I, [_P]),
     "pir_engine_stream": (_P, [_P]),
@@ -86,7 +87,7 @@ PROTOTYPES = {
     "pir_engine_set_profiling": (_I, [_P, _I]),
     "pir_engine_last_timings": (_I, [_P, ctypes.POINTER(PirKernelTime), _I]),
     "pir_engine_profile_phases": (_I, [_P, _P, _I, ctypes.POINTER(ctypes.c_float)]),
-    "pir_engine_trace_query": (_I, [_P, _P, _P, _I]),
+    "pir_engine_trace_query": (_I, [_P, _P, _I, _P, _I]),
     "pir_comm_unique_id": (_I, [_P]),
     "pir_comm_attach": (_I, [_P, _P, _I, _I]),
     # pir_client.h

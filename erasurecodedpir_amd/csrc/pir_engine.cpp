@@ -233,13 +233,14 @@ int answer_fused(pir_engine* e, const uint8_t* d_raw, int log_parts_total, uint6
   return PIR_OK;
 }
 
-// one launch: key parse, tree and scan in k_query; then the slab reduce
-int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw,
+// one launch: key parse, tree and scan of nk queued keys (key_len apart) in k_query; then the
+// slab reduce of all nk answers (d_out: nk x nq x efs)
+int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, int nk,
                  int log_parts_total, uint64_t prefix, uint64_t row0, uint8_t* d_out,
                  hipStream_t s) {
   const auto& c = e->cfg;
   const pir::ScanShape& sh = qp.shape;
-  int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
+  int rc = ensure_slabs(e, (size_t)nk * pir::query_slab_bytes(qp));
   if (rc) return rc;
   e->last_chunks = 1;
   e->last_fused = 2;
@@ -251,13 +252,14 @@ int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw,
     HIP_TRY(hipEventRecord(ev[EV_LEAF_E], s));
     HIP_TRY(hipEventRecord(ev[EV_SCAN_B], s));
   }
-  HIP_TRY(pir::launch_query(qp, d_raw, c.num_parties, c.log_num_records, c.party_index - 1,
-                            log_parts_total, prefix, e->d_shard + row0 * e->pitch, e->d_slabs, s));
+  HIP_TRY(pir::launch_query(qp, d_raw, (uint32_t)e->key_len, nk, c.num_parties,
+                            c.log_num_records, c.party_index - 1, log_parts_total, prefix,
+                            e->d_shard + row0 * e->pitch, e->d_slabs, s));
   if (ev) {
     HIP_TRY(hipEventRecord(ev[EV_SCAN_E], s));
     HIP_TRY(hipEventRecord(ev[EV_PRERED], s));
   }
-  HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, d_out, s));
+  HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, d_out, s, nk));
   if (ev) HIP_TRY(hipEventRecord(ev[EV_RED], s));
   return PIR_OK;
 }
@@ -270,7 +272,7 @@ int answer_core(pir_engine* e, const uint8_t* d_raw, int log_parts_total, uint64
   if (e->allow_query && e->allow_fused) {
     const pir::QueryPlan qp = pir::make_query_plan(c.log_num_records, log_parts_total,
                                                    c.num_parties, c.num_rounds, e->pitch, e->num_cus);
-    if (qp.tile) return answer_query(e, qp, d_raw, log_parts_total, prefix, row0, d_out, s);
+    if (qp.tile) return answer_query(e, qp, d_raw, 1, log_parts_total, prefix, row0, d_out, s);
   }
   const int tile = e->allow_fused ? pir::fused_tile(c.num_rounds, e->pitch, nleaves, e->num_cus) : 0;
   if (tile) return answer_fused(e, d_raw, log_parts_total, prefix, row0, d_out, s, tile);
@@ -504,6 +506,51 @@ int answer_batch_locked(pir_engine* e, const uint8_t* d_keys, int nk, uint8_t* d
   return PIR_OK;
 }
 
+// nk independent queries, each its own tree and full shard pass, answered back to back: one
+// k_query launch when the shape allows (the tree of query k+1 overlaps the scan of query k),
+// else one answer after another.  d_result: nk x nq x efs.
+int answer_stream_locked(pir_engine* e, const uint8_t* d_keys, int nk, uint8_t* d_result,
+                         hipStream_t s) {
+  const auto& c = e->cfg;
+  const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
+  e->ev = nullptr;
+  if (nk == 0) return PIR_OK;
+  const pir::QueryPlan qp = pir::make_query_plan(c.log_num_records, c.log_num_partitions,
+                                                 c.num_parties, c.num_rounds, e->pitch, e->num_cus,
+                                                 nk);
+  if (c.is_byzantine || !qp.tile || !e->allow_query || !e->allow_fused) {
+    for (int k = 0; k < nk; ++k) {
+      int rc = answer_dev_locked(e, d_keys + (size_t)k * e->key_len, d_result + k * out_bytes, s);
+      if (rc) return rc;
+    }
+    return PIR_OK;
+  }
+  const size_t total = out_bytes * nk;
+  uint8_t* part_out = d_result;
+  if (e->comm) {
+    int rc = ensure_buf(&e->d_bpart, &e->bpart_cap, total);
+    if (!rc) rc = ensure_buf(&e->d_bgather, &e->bgather_cap, total * e->nranks);
+    if (rc) return rc;
+    part_out = e->d_bpart;
+  }
+  if (!e->prof.empty()) {  // one event set for the whole queue (phases of the one launch)
+    e->ev = e->prof[e->prof_next].ev;
+    e->prof_next = (e->prof_next + 1) % (int)e->prof.size();
+    e->prof_count = std::min(e->prof_count + 1, (int)e->prof.size());
+    HIP_TRY(hipEventRecord(e->ev[EV_START], s));
+  }
+  int rc = answer_query(e, qp, d_keys, nk, c.log_num_partitions, (uint64_t)c.partition_index, 0,
+                        part_out, s);
+  if (rc) return rc;
+  if (e->comm) {
+    RCCL_TRY(ncclAllGather(e->d_bpart, e->d_bgather, total, ncclUint8, e->comm, s));
+    HIP_TRY(pir::launch_xor_fold(e->d_bgather, e->nranks, total, d_result, s));
+  }
+  if (e->ev) HIP_TRY(hipEventRecord(e->ev[EV_END], s));
+  e->ev = nullptr;
+  return PIR_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -733,6 +780,16 @@ int pir_engine_answer_batch(pir_engine_t* e, const uint8_t* keys, int num_keys,
   return rc;
 }
 
+int pir_engine_answer_stream_dev(pir_engine_t* e, const uint8_t* d_keys, int num_keys,
+                                 uint8_t* d_result, void* stream) {
+  if (!e || !d_result || num_keys < 0) return fail(PIR_EINVAL, "bad argument");
+  if (int rc = check_key_ptr(d_keys)) return rc;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  return answer_stream_locked(e, d_keys, num_keys, d_result, s);
+}
+
 int pir_engine_set_batch_group(pir_engine_t* e, int keys_per_pass) {
   if (!e || keys_per_pass < 0 || keys_per_pass > 16) return fail(PIR_EINVAL, "bad argument");
   e->batch_group = keys_per_pass;
@@ -902,16 +959,18 @@ int pir_engine_profile_phases(pir_engine_t* e, const uint8_t* d_key, int iters, 
   return PIR_OK;
 }
 
-int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, uint64_t* out, int max_wgs) {
-  if (!e || !d_key || !out || max_wgs < 0) return fail(PIR_EINVAL, "bad argument");
+int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, int num_keys, uint64_t* out,
+                           int max_wgs) {
+  if (!e || !d_key || !out || max_wgs < 0 || num_keys < 1) return fail(PIR_EINVAL, "bad argument");
   std::lock_guard<std::mutex> lk(e->mu);
   const auto& c = e->cfg;
   HIP_TRY(hipSetDevice(c.device));
   const pir::QueryPlan qp = pir::make_query_plan(c.log_num_records, c.log_num_partitions,
-                                                 c.num_parties, c.num_rounds, e->pitch, e->num_cus);
+                                                 c.num_parties, c.num_rounds, e->pitch, e->num_cus,
+                                                 num_keys);
   if (!qp.tile) return fail(PIR_EINVAL, "shape does not use the single-launch query kernel");
   const pir::ScanShape& sh = qp.shape;
-  int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
+  int rc = ensure_slabs(e, (size_t)num_keys * pir::query_slab_bytes(qp));
   if (rc) return rc;
   const int nwg = (int)sh.grid.x;
   const size_t bytes = (size_t)nwg * pir::kQueryTraceSlots * sizeof(uint64_t);
@@ -920,9 +979,9 @@ int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, uint64_t* out,
   std::vector<uint64_t> h((size_t)nwg * pir::kQueryTraceSlots);
   hipError_t err = hipMemsetAsync(d_tr, 0, bytes, e->stream);
   if (err == hipSuccess)
-    err = pir::launch_query(qp, d_key, c.num_parties, c.log_num_records, c.party_index - 1,
-                            c.log_num_partitions, (uint64_t)c.partition_index, e->d_shard,
-                            e->d_slabs, e->stream, d_tr);
+    err = pir::launch_query(qp, d_key, (uint32_t)e->key_len, num_keys, c.num_parties, c.log_num_records,
+                            c.party_index - 1, c.log_num_partitions, (uint64_t)c.partition_index,
+                            e->d_shard, e->d_slabs, e->stream, d_tr);
   if (err == hipSuccess) err = hipMemcpyAsync(h.data(), d_tr, bytes, hipMemcpyDeviceToHost, e->stream);
   if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
   (void)hipFree(d_tr);
@@ -933,7 +992,8 @@ int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, uint64_t* out,
   for (int w = 0; w < n; ++w)
     for (int k = 0; k < pir::kQueryTraceSlots; ++k) {
       const uint64_t v = h[(size_t)w * pir::kQueryTraceSlots + k];
-      out[(size_t)w * pir::kQueryTraceSlots + k] = k >= 56 ? v : (v ? v - t0 : 0);
+      const bool clk = k == 56 || k == 57 || k >= 128;  // shader-clock ticks, not wall time
+      out[(size_t)w * pir::kQueryTraceSlots + k] = clk ? v : (v ? v - t0 : 0);
     }
   return nwg;
 }

@@ -105,20 +105,28 @@ ScanShape make_fused_shape(uint64_t nleaves, uint32_t pitch, int nq, int num_cus
 hipError_t launch_fused(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb,
                         const uint8_t* shard, const ScanShape& sh, uint8_t* slabs, int tile,
                         hipStream_t s);
-// Single-launch query (k_query): key parse + whole tree + scan in one persistent launch of
-// 2^lr workgroups, each owning 2^lt tiles of `tile` leaves.  tile == 0: shape not supported.
+// Single-launch queries (k_query): key parse + whole tree + scan in one persistent launch of
+// 2^lr workgroups, each owning 2^lt tiles of `tile` leaves, for a queue of nk keys (raw keys
+// key_stride bytes apart; query k's slabs at d_slabs + k * query_slab_bytes(qp)).
+// tile == 0: shape not supported.
 struct QueryPlan {
   int tile, lr, lt;
   ScanShape shape;  // grid.x = 2^lr workgroups (slabs), grid.y = column groups
 };
-QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, int num_cus);
-constexpr int kQueryTraceSlots = 64;  // trace: per-workgroup phase stamps (wall clock, 100 MHz)
-hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, int p, int n, int party0,
-                        int log_parts, uint64_t prefix, const uint8_t* shard, uint8_t* slabs,
-                        hipStream_t s, uint64_t* trace = nullptr);
-// XOR the slabs, compact pitch -> record_bytes: d_out[a*efs + b]
+QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, int num_cus,
+                          int nk = 1);
+inline size_t query_slab_bytes(const QueryPlan& qp) {
+  return (size_t)qp.shape.grid.x * qp.shape.grid.y * qp.shape.slab_bytes;
+}
+constexpr int kQueryTraceSlots = 160;  // trace: per-workgroup phase stamps (wall clock, 100 MHz)
+hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
+                        int p, int n, int party0, int log_parts, uint64_t prefix,
+                        const uint8_t* shard, uint8_t* slabs, hipStream_t s,
+                        uint64_t* trace = nullptr);
+// XOR the slabs, compact pitch -> record_bytes: d_out[a*efs + b]; nk queries (slabs of query k
+// grid.x*grid.y*slab_bytes apart, answers nq*efs bytes apart)
 hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t efs,
-                         uint8_t* d_out, hipStream_t s);
+                         uint8_t* d_out, hipStream_t s, int nk = 1);
 // d_out[i] = XOR_r d_in[r*len + i]
 hipError_t launch_xor_fold(const uint8_t* d_in, int nranks, size_t len, uint8_t* d_out,
                            hipStream_t s);

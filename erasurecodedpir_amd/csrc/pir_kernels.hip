@@ -443,6 +443,11 @@ __device__ __forceinline__ uint4 load_coef(const uint8_t* c, uint64_t i) {
   }
 }
 
+// z ^ (x & m) in one v_bitop3 (m an all-ones / all-zeros mask, wave-uniform in an SGPR)
+__device__ __forceinline__ uint32_t mxor(uint32_t z, uint32_t x, uint32_t m) {
+  return __builtin_amdgcn_bitop3_b32(z, x, m, 0x78);
+}
+
 __device__ __forceinline__ uint32_t coef_byte(const uint4& c, int a) {
   const uint32_t w = a < 4 ? c.x : (a < 8 ? c.y : (a < 12 ? c.z : c.w));
   return (w >> (8 * (a & 3))) & 0xffu;
@@ -765,13 +770,20 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
 #pragma unroll
             for (int a = 0; a < NQ; ++a) {
               const uint32_t ca = coef_byte(cf[u], a);
-              if (UNI) {  // scalar branches: ~4 XORs per dword instead of 8 masked ones
+              if (UNI && NQ <= 2) {  // scalar branches: ~4 XORs per dword instead of 8 masked
 #pragma unroll
                 for (int kk = 0; kk < 8; ++kk)
                   if (ca & (1u << kk)) {
 #pragma unroll
                     for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= x[u].v[v];
                   }
+              } else if (UNI) {  // many rounds: branch-free, SGPR masks (no 8*NQ branches)
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk) {
+                  const uint32_t m = 0u - ((ca >> kk) & 1u);
+#pragma unroll
+                  for (int v = 0; v < VEC; ++v) Z[a][kk][v] = mxor(Z[a][kk][v], x[u].v[v], m);
+                }
               } else {
 #pragma unroll
                 for (int kk = 0; kk < 8; ++kk) {
@@ -806,36 +818,41 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
 }
 
 // ------------------------------------------------------------------------------------------
-// k_query: ONE launch answers one query (no frontier / expand kernels before it).  Workgroup b
-// owns region b of the partition (R = 2^(nr - lr) leaves, nr = n - log_parts) = T tiles of
-// TILE leaves.  Tree waves:
-//   * key: every workgroup parses the correction words of all levels into LDS;
+// k_query: ONE launch answers a queue of `nk` independent queries, each its own DPF tree and
+// its own full pass over the shard (no frontier / expand kernels before it).  Workgroup b owns
+// region b of the partition (R = 2^(nr - lr) leaves, nr = n - log_parts) = T tiles of TILE
+// leaves, and walks the tiles of query 0, then of query 1, ... .  Tree waves:
+//   * key: the correction words of all levels and lastCW of the current query, in LDS;
 //   * tile root: wave 0 walks the tree depth-first in column shape (16 lanes per node) from the
-//     root along (prefix, b, tile) -- the first tile descends all Lt = log_parts + lr + log2 T
-//     levels; tile i > 0 pops the right sibling stored when its ancestor was expanded and
-//     descends ctz(i) levels, so the T tile roots cost T - 1 expansions in all;
-//   * tile: expand the root breadth-first in LDS, column shape while a level has <= 32 nodes
-//     (latency), row shape below (throughput), and write the DPF shares into the LDS ring.
-// Scan waves are k_fused's.  The first scan starts after Lt + log2 TILE dependent AES levels.
+//     root along (prefix, b, tile) -- tile 0 descends all Lt = log_parts + lr + log2 T levels;
+//     tile i > 0 pops the right sibling stored when its ancestor was expanded and descends
+//     ctz(i) levels, so the T tile roots cost T - 1 expansions in all;
+//   * tile: expand the root breadth-first in LDS and write the DPF shares into the LDS ring
+//     (RING slots, so the tree runs up to RING - 1 tiles ahead of the scan).
+// Tile 0 of query 0 is built by all 16 waves (nothing to scan before it).  Later tiles -- and
+// the descent and first tile of the next query -- are built by the TW tree waves while the
+// scan waves stream the previous ones, so in a queue only the first query waits for its tree.
+// Scan waves are k_fused's; at the end of a query they fold their bit planes into LDS and
+// write the workgroup's partial answer (slab) of that query.
 // ------------------------------------------------------------------------------------------
 constexpr int kQueryCwCap = 256;  // (levels x (p-1)) correction words staged in LDS
 
-template <int TILE, int NRP, int NQ, int VEC, int GYMAX>
+template <int TILE, int NRP, int NQ, int VEC, int GYMAX, int RING>
 struct QuerySmem {
   uint32_t tab[2 * 256 * 32];
   uint4 sa[TILE / 2];
   uint32_t ta[TILE / 2];
   uint4 sb[TILE / 4];
   uint32_t tb[TILE / 4];
-  uint8_t ring[2][TILE * NRP];
+  uint8_t ring[RING][TILE * NRP];
   uint32_t red[GYMAX][NQ * kColGroupLanes * VEC];
   uint4 scw[kQueryCwCap];           // sCW[L][j] at L * (p-1) + j
   uint32_t tcw[kQueryCwCap];
   uint4 lastcw[kMaxCW];
   uint4 stk_s[kMaxLevels + 1];      // right siblings on the current root-to-tile path
   uint32_t stk_t[kMaxLevels + 1];
-  uint32_t bar, ready;
-  uint32_t consumed[2];
+  uint32_t bar, sbar, ready;
+  uint32_t consumed[RING];
 };
 
 __device__ __forceinline__ void cw_lds(const uint4* scw, const uint32_t* tcw, int L, uint32_t t,
@@ -850,39 +867,49 @@ __device__ __forceinline__ void cw_lds(const uint4* scw, const uint32_t* tcw, in
   }
 }
 
-template <int NQ, int NRP, int VEC, bool UNI, int TW, int TILE, int GYMAX>
+// the key's correction words (dpf_tree.cpp:504-519) into LDS, by threads [0, nt)
+__device__ __forceinline__ void stage_key(const uint8_t* __restrict__ raw, int p, int n, int nq,
+                                          int tid, int nt, uint4* scw, uint32_t* tcw,
+                                          uint4* lastcw) {
+  const int pm1 = p - 1;
+  for (int i = tid; i < n * pm1; i += nt) {
+    const int L = i / pm1, j = i - L * pm1;
+    parse_cw(raw, p, L, j, scw[i], tcw[i]);
+  }
+  for (int j = tid; j < kMaxCW; j += nt) {
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (j < pm1)
+      for (int a = 0; a < nq; ++a)
+        w[a >> 2] |= (uint32_t)raw[16 + n * pm1 * (16 + 2 * p - 2) + a * pm1 + j] << (8 * (a & 3));
+    lastcw[j] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+template <int NQ, int NRP, int VEC, bool UNI, int TW, int TILE, int GYMAX, int RING>
 __global__ __launch_bounds__(kFusedThreads) void k_query(
-    const uint8_t* __restrict__ raw, int p, int n, int nq, int party0, int log_parts,
-    uint64_t prefix, int lr, int lt, const uint8_t* __restrict__ shard, uint32_t pitch,
-    uint32_t cpr, uint32_t gy, uint8_t* __restrict__ slabs, uint64_t* __restrict__ trace) {
-  // trace != nullptr: per-workgroup wall-clock stamps (100 MHz) of the phases, kQueryTraceSlots
-  // apart: start, key parsed, first tile root, tile 0 ready, last tile ready, scan done, end
+    const uint8_t* __restrict__ raw0, uint32_t key_stride, int nk, int p, int n, int nq,
+    int party0, int log_parts, uint64_t prefix, int lr, int lt, const uint8_t* __restrict__ shard,
+    uint32_t pitch, uint32_t cpr, uint32_t gy, uint8_t* __restrict__ slabs,
+    uint64_t* __restrict__ trace) {
+  // trace != nullptr: per-workgroup wall-clock stamps (100 MHz) of query 0's phases,
+  // kQueryTraceSlots apart (layout: pir_engine_trace_query, include/pir_engine.h)
   if (trace) trace += (uint64_t)blockIdx.x * kQueryTraceSlots;
   if (trace && threadIdx.x == 0) { trace[0] = wall_clock64(); trace[56] = clock64(); }
   constexpr int SW = kFusedWaves - TW;
   constexpr int CH = VEC * 4;
   constexpr int GW = kColGroupLanes * VEC;
-  constexpr int NW = NRP <= 4 ? 1 : NRP / 4;
   constexpr int KT = TILE == 4096 ? 12 : 10;  // log2 TILE
-  using Smem = QuerySmem<TILE, NRP, NQ, VEC, GYMAX>;
+  using Smem = QuerySmem<TILE, NRP, NQ, VEC, GYMAX, RING>;
   static_assert(sizeof(Smem) <= 160 * 1024, "LDS");
   __shared__ Smem sm;
   const uint32_t pm1 = (uint32_t)p - 1;
   load_tables_n<kFusedThreads>(sm.tab);
   for (int i = threadIdx.x; i < GYMAX * NQ * GW; i += blockDim.x) (&sm.red[0][0])[i] = 0;
-  // the key (dpf_tree.cpp:504-519): CWs of every level, lastCW (k_key_prep's layout, in LDS)
-  for (int i = threadIdx.x; i < n * (int)pm1; i += blockDim.x) {
-    const int L = i / (int)pm1, j = i - L * (int)pm1;
-    parse_cw(raw, p, L, j, sm.scw[i], sm.tcw[i]);
+  stage_key(raw0, p, n, nq, threadIdx.x, kFusedThreads, sm.scw, sm.tcw, sm.lastcw);
+  if (threadIdx.x == 0) {
+    sm.bar = 0; sm.sbar = 0; sm.ready = 0;
+    for (int r = 0; r < RING; ++r) sm.consumed[r] = 0;
   }
-  for (int j = threadIdx.x; j < kMaxCW; j += blockDim.x) {
-    uint32_t w[4] = {0, 0, 0, 0};
-    if (j < (int)pm1)
-      for (int a = 0; a < nq; ++a)
-        w[a >> 2] |= (uint32_t)raw[16 + n * (int)pm1 * (16 + 2 * p - 2) + a * (int)pm1 + j] << (8 * (a & 3));
-    sm.lastcw[j] = make_uint4(w[0], w[1], w[2], w[3]);
-  }
-  if (threadIdx.x == 0) { sm.bar = 0; sm.ready = 0; sm.consumed[0] = 0; sm.consumed[1] = 0; }
   __syncthreads();
   if (trace && threadIdx.x == 0) trace[1] = wall_clock64();
 
@@ -890,12 +917,14 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t b = blockIdx.x;
   const uint32_t ntiles = 1u << lt;
+  const uint32_t total = ntiles * (uint32_t)nk;  // tiles of the whole queue
   const uint64_t region_rows = (uint64_t)TILE << lt;
+  const size_t slab_words = (size_t)NQ * GW;
+  const size_t slab_q_words = (size_t)gy * gridDim.x * slab_words;  // one query's slabs
 
   // ======================================= tree work =======================================
-  // tree_tile(i, nt, team): the shares of tile i into ring slot i&1, by the first nt threads
-  // (team = their waves).  Tile 0 is built by all 16 waves (the scan waves have nothing to
-  // read before it); later tiles by the TW tree waves while the scan waves stream.
+  // tree_tile(g, nt, team): the shares of queue tile g (query g / T, tile g % T) into ring slot
+  // g % RING, by the first nt threads (team = their waves)
   const Tab T(sm.tab);
   const Bits B((uint32_t)p);
   const int tt = threadIdx.x;
@@ -918,14 +947,20 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
   auto cw = [&](int L, uint32_t tv, uint4& cs, uint32_t& ct) {
     cw_lds(sm.scw, sm.tcw, L, tv, pm1, cs, ct);
   };
-  auto tree_tile = [&](uint32_t i, int nt, uint32_t team) {
-    uint8_t* ring = sm.ring[i & 1];
+  auto tree_tile = [&](uint32_t g, int nt, uint32_t team) {
+    const uint32_t i = g % ntiles;
+    const uint8_t* raw = raw0 + (size_t)(g / ntiles) * key_stride;
+    uint8_t* ring = sm.ring[g % RING];
     // the whole workgroup: hardware barrier (waiting waves sleep); the tree waves alone: LDS
     // counter barrier (the scan waves keep streaming)
     auto sync = [&]() {
       if (team == (uint32_t)kFusedWaves) __syncthreads();
       else group_barrier(&sm.bar, gen, team);
     };
+    if (i == 0 && g > 0) {  // next query: its key replaces the previous one's (all tree waves
+      stage_key(raw, p, n, nq, tt, nt, sm.scw, sm.tcw, sm.lastcw);  // are past its last use)
+      sync();
+    }
     // ---- tile root (wave 0, column shape, depth-first) ------------------------------------
     if (wave == 0) {
       int L0, depth;
@@ -973,13 +1008,13 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
         const uint32_t c3 = __builtin_amdgcn_readlane(oc, (int)(4 * bit + 3));
         sq = (c0 & m0) | (c1 & m1) | (c2 & m2) | (c3 & m3);
         t = (tbits >> (bit * pm1)) & B.tmask;
-        if (trace && i == 0 && lane == 0 && d < 32) trace[8 + d] = wall_clock64();
+        if (trace && g == 0 && lane == 0 && d < 32) trace[8 + d] = wall_clock64();
       }
       uint4* s0 = ((KT - 1) & 1) ? sm.sb : sm.sa;
       uint32_t* t0 = ((KT - 1) & 1) ? sm.tb : sm.ta;
       if (lane < 4) reinterpret_cast<uint32_t*>(&s0[0])[lane] = sq;
       if (lane == 0) t0[0] = t;
-      if (trace && i == 0 && lane == 0) { trace[2] = wall_clock64(); trace[57] = clock64(); }
+      if (trace && g == 0 && lane == 0) { trace[2] = wall_clock64(); trace[57] = clock64(); }
     }
     sync();
     // ---- breadth-first expansion of the tile root ------------------------------------------
@@ -1008,9 +1043,9 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
             ot[2 * u + 1] = (tb >> B.pm1) & B.tmask;
           }
         }
-      } else if (team == (uint32_t)kFusedWaves) {
-        // 3 lanes per node, lane r runs CTR block r with its own key schedule: a third of the
-        // row-shape latency when the whole workgroup expands a narrow-ish level (tile 0)
+      } else if (W <= (nt >> 6) * 21) {
+        // 3 lanes per node, lane r runs CTR block r with its own key schedule: two thirds of
+        // the row-shape latency for a level that fits the team in one pass
         const int l = tt & 63, ul = l / 3, r = l - 3 * ul;
         const int npp = (nt >> 6) * 21;
         for (int u = (tt >> 6) * 21 + ul; l < 63 && u < W; u += npp) {
@@ -1041,78 +1076,84 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
         }
       }
       sync();
-      if (trace && i == 0 && tt == 0 && lv < 16) trace[40 + lv] = wall_clock64();
+      if (trace && g == 0 && tt == 0 && lv < 16) trace[40 + lv] = wall_clock64();
       buf ^= 1;
       W *= 2;
     }
-    if (team == (uint32_t)kFusedWaves) {  // last level + leaves, 3 lanes per parent
+    // ---- last level + leaf conversion (dpf_tree.cpp:567-580) into the ring -----------------
+    // c[leaf][a] = AES_{s_leaf}(0)[a] ^ XOR_{k: t_leaf bit k} lastCW[k][a]   (a < nq)
+    {
       const uint4* is = buf ? sm.sb : sm.sa;
       const uint32_t* it = buf ? sm.tb : sm.ta;
-      const int l = tt & 63, ul = l / 3, r = l - 3 * ul;
-      const int npp = (nt >> 6) * 21;
-      const int u0 = (tt >> 6) * 21 + ul;
-      const int src = (l < 63 ? l - r + 2 : l);  // the node's control-bit lane
-      for (int ub = 0; ub < W; ub += npp) {  // uniform trip count: every lane joins the shuffle
-        const int u = u0 + ub;
-        const bool act = l < 63 && u < W;
-        uint4 cs = make_uint4(0, 0, 0, 0);
-        uint32_t ct = 0;
-        uint4 o = make_uint4(0, 0, 0, 0);
-        if (act) {
+      if (team == (uint32_t)kFusedWaves) {  // 3 lanes per parent; the child lanes convert
+        const int l = tt & 63, ul = l / 3, r = l - 3 * ul;
+        const int npp = (nt >> 6) * 21;
+        const int u0 = (tt >> 6) * 21 + ul;
+        const int src = (l < 63 ? l - r + 2 : l);  // the node's control-bit lane
+        for (int ub = 0; ub < W; ub += npp) {  // uniform trip count: every lane joins the shuffle
+          const int u = u0 + ub;
+          const bool act = l < 63 && u < W;
+          uint4 cs = make_uint4(0, 0, 0, 0);
+          uint32_t ct = 0;
+          uint4 o = make_uint4(0, 0, 0, 0);
+          if (act) {
+            cw(L_leaf_parent, it[u], cs, ct);
+            o = aes_ctr_block(T, is[u], (uint32_t)r);
+          }
+          const uint32_t tb = (uint32_t)__shfl((int)((o.x & B.tb_mask) ^ ct), src, 64);
+          if (act && r < 2) {
+            const uint32_t tc = (tb >> (r * pm1)) & B.tmask;
+            uint4 v = aes_ctr_block(T, xor4(o, cs), 0u);
+            for (uint32_t j = 0; j < pm1; ++j) v = xor4(v, and4(sm.lastcw[j], 0u - ((tc >> j) & 1u)));
+            store_leaf<NRP>(ring, 2 * u + r, make_uint4(v.x & qm.x, v.y & qm.y, v.z & qm.z, v.w & qm.w));
+          }
+        }
+      } else {
+        constexpr int NW = NRP <= 4 ? 1 : NRP / 4;
+        for (int u = tt; u < W; u += nt) {
+          uint4 cs;
+          uint32_t ct;
           cw(L_leaf_parent, it[u], cs, ct);
-          o = aes_ctr_block(T, is[u], (uint32_t)r);
-        }
-        const uint32_t tb = (uint32_t)__shfl((int)((o.x & B.tb_mask) ^ ct), src, 64);
-        if (act && r < 2) {
-          const uint32_t tc = (tb >> (r * pm1)) & B.tmask;
-          uint4 v = aes_ctr_block(T, xor4(o, cs), 0u);
-          for (uint32_t j = 0; j < pm1; ++j) v = xor4(v, and4(sm.lastcw[j], 0u - ((tc >> j) & 1u)));
-          store_leaf<NRP>(ring, 2 * u + r, make_uint4(v.x & qm.x, v.y & qm.y, v.z & qm.z, v.w & qm.w));
-        }
-      }
-    } else {  // last level + leaf conversion (dpf_tree.cpp:567-580) into the ring
-      const uint4* is = buf ? sm.sb : sm.sa;
-      const uint32_t* it = buf ? sm.tb : sm.ta;
-      for (int u = tt; u < W; u += nt) {
-        uint4 cs;
-        uint32_t ct;
-        cw(L_leaf_parent, it[u], cs, ct);
-        uint4 o[3];
-        aes_ctr_row<3, 1>(T, is[u], o);
-        const uint32_t tb = (o[2].x & B.tb_mask) ^ ct;
-        const uint32_t tl = tb & B.tmask, tr = (tb >> B.pm1) & B.tmask;
-        uint4 vl[1], vr[1];
-        aes_ctr_row<1, NW>(T, xor4(o[0], cs), vl);
-        aes_ctr_row<1, NW>(T, xor4(o[1], cs), vr);
-        for (uint32_t j = 0; j < pm1; ++j) {
-          vl[0] = xor4(vl[0], and4(sm.lastcw[j], 0u - ((tl >> j) & 1u)));
-          vr[0] = xor4(vr[0], and4(sm.lastcw[j], 0u - ((tr >> j) & 1u)));
-        }
-        const uint4 a = make_uint4(vl[0].x & qm.x, vl[0].y & qm.y, vl[0].z & qm.z, vl[0].w & qm.w);
-        const uint4 c = make_uint4(vr[0].x & qm.x, vr[0].y & qm.y, vr[0].z & qm.z, vr[0].w & qm.w);
-        if constexpr (NRP == 1) {
-          *reinterpret_cast<uint16_t*>(ring + 2 * u) = (uint16_t)((a.x & 0xffu) | ((c.x & 0xffu) << 8));
-        } else {
-          store_leaf<NRP>(ring, 2 * u, a);
-          store_leaf<NRP>(ring, 2 * u + 1, c);
+          uint4 o[3];
+          aes_ctr_row<3, 1>(T, is[u], o);
+          const uint32_t tb = (o[2].x & B.tb_mask) ^ ct;
+          const uint32_t tl = tb & B.tmask, tr = (tb >> B.pm1) & B.tmask;
+          uint4 vl[1], vr[1];
+          aes_ctr_row<1, NW>(T, xor4(o[0], cs), vl);
+          aes_ctr_row<1, NW>(T, xor4(o[1], cs), vr);
+          for (uint32_t j = 0; j < pm1; ++j) {
+            vl[0] = xor4(vl[0], and4(sm.lastcw[j], 0u - ((tl >> j) & 1u)));
+            vr[0] = xor4(vr[0], and4(sm.lastcw[j], 0u - ((tr >> j) & 1u)));
+          }
+          const uint4 a = make_uint4(vl[0].x & qm.x, vl[0].y & qm.y, vl[0].z & qm.z, vl[0].w & qm.w);
+          const uint4 c = make_uint4(vr[0].x & qm.x, vr[0].y & qm.y, vr[0].z & qm.z, vr[0].w & qm.w);
+          if constexpr (NRP == 1) {
+            *reinterpret_cast<uint16_t*>(ring + 2 * u) = (uint16_t)((a.x & 0xffu) | ((c.x & 0xffu) << 8));
+          } else {
+            store_leaf<NRP>(ring, 2 * u, a);
+            store_leaf<NRP>(ring, 2 * u + 1, c);
+          }
         }
       }
     }
-    sync();  // every share of tile i is in the ring
+    sync();  // every share of tile g is in the ring
     if (wave == 0) lds_signal(&sm.ready);
-    if (trace && tt == 0 && (i == 0 || i == ntiles - 1)) trace[i == 0 ? 3 : 4] = wall_clock64();
+    if (trace && tt == 0 && (g == 0 || g == ntiles - 1)) trace[g == 0 ? 3 : 4] = wall_clock64();
+    if (trace && tt == 0 && g < 32) { trace[64 + g] = wall_clock64(); trace[128 + g] = clock64(); }
   };
 
   tree_tile(0, kFusedThreads, kFusedWaves);  // every wave builds the first tile
   if (wave < (uint32_t)TW) {
     // ===================================== tree role ======================================
-    for (uint32_t i = 1; i < ntiles; ++i) {
-      if (i >= 2) lds_wait_geq(&sm.consumed[i & 1], (i >> 1) * SW);
-      tree_tile(i, TW * 64, TW);
+    for (uint32_t g = 1; g < total; ++g) {
+      // slot g % RING free: every scan wave has consumed tile g - RING (per-slot counts)
+      if (g >= (uint32_t)RING) lds_wait_geq(&sm.consumed[g % RING], (g / RING) * SW);
+      tree_tile(g, TW * 64, TW);
     }
   } else {
     // ===================================== scan role ======================================
     const uint32_t sw = wave - TW;
+    uint32_t sgen = 0;  // scan-wave barrier generation
     uint32_t gcol, wi, nwg, rpw, rec_off, chunk;
     bool active;
     if (UNI) {
@@ -1140,9 +1181,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
     constexpr int U = SW >= 8 ? 8 : 16;
     __builtin_amdgcn_s_setprio(2);
     const uint8_t* rbase = shard + (b * region_rows) * pitch + (uint64_t)chunk * CH;
-    for (uint32_t i = 0; i < ntiles; ++i) {
-      const uint8_t* ring = sm.ring[i & 1];
-      lds_wait_geq(&sm.ready, i + 1);
+    for (uint32_t g = 0; g < total; ++g) {
+      const uint32_t i = g % ntiles;
+      const uint8_t* ring = sm.ring[g % RING];
+      lds_wait_geq(&sm.ready, g + 1);
       if (wi < nwg) {
         const uint8_t* base = rbase + ((uint64_t)i * TILE) * pitch;
         for (uint32_t g0 = wi; g0 < ngroups; g0 += U * nwg) {
@@ -1170,13 +1212,20 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
 #pragma unroll
             for (int a = 0; a < NQ; ++a) {
               const uint32_t ca = coef_byte(cf[u], a);
-              if (UNI) {
+              if (UNI && NQ <= 2) {
 #pragma unroll
                 for (int kk = 0; kk < 8; ++kk)
                   if (ca & (1u << kk)) {
 #pragma unroll
                     for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= x[u].v[v];
                   }
+              } else if (UNI) {
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk) {
+                  const uint32_t m = 0u - ((ca >> kk) & 1u);
+#pragma unroll
+                  for (int v = 0; v < VEC; ++v) Z[a][kk][v] = mxor(Z[a][kk][v], x[u].v[v], m);
+                }
               } else {
 #pragma unroll
                 for (int kk = 0; kk < 8; ++kk) {
@@ -1188,36 +1237,56 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
             }
         }
       }
-      lds_signal(&sm.consumed[i & 1]);
-    }
-    if (trace && sw == 0 && lane == 0) trace[5] = wall_clock64();
-    if (active) {
-      const uint32_t wbase = (UNI ? lane : chunk) * VEC;
+      lds_signal(&sm.consumed[g % RING]);
+      if (trace && sw == 0 && lane == 0 && g < 32) trace[96 + g] = wall_clock64();
+      if (i == ntiles - 1) {  // end of a query: sum_k alpha^k Z_k into LDS, then the slab
+        const uint32_t qy = g / ntiles;
+        if (trace && qy == 0 && sw == 0 && lane == 0) trace[5] = wall_clock64();
+        if (active) {
+          const uint32_t wbase = (UNI ? lane : chunk) * VEC;
 #pragma unroll
-      for (int a = 0; a < NQ; ++a)
+          for (int a = 0; a < NQ; ++a)
 #pragma unroll
-        for (int v = 0; v < VEC; ++v) {
-          uint32_t acc = Z[a][7][v];
+            for (int v = 0; v < VEC; ++v) {
+              uint32_t acc = Z[a][7][v];
 #pragma unroll
-          for (int kk = 6; kk >= 0; --kk) acc = gf_xtime4(acc) ^ Z[a][kk][v];
-          if (acc) atomicXor(&sm.red[gcol][a * GW + wbase + v], acc);
+              for (int kk = 6; kk >= 0; --kk) acc = gf_xtime4(acc) ^ Z[a][kk][v];
+              if (acc) atomicXor(&sm.red[gcol][a * GW + wbase + v], acc);
+            }
         }
+#pragma unroll
+        for (int a = 0; a < NQ; ++a)
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) Z[a][kk][v] = 0;
+        group_barrier(&sm.sbar, sgen, SW);  // every scan wave's planes are in red[]
+        uint32_t* qslab = reinterpret_cast<uint32_t*>(slabs) + qy * slab_q_words;
+        const int st = (int)threadIdx.x - TW * 64;
+        for (uint32_t gg = 0; gg < gy; ++gg) {
+          uint32_t* slab = qslab + ((uint64_t)gg * gridDim.x + blockIdx.x) * slab_words;
+          for (int k = st; k < (int)slab_words; k += SW * 64) {
+            slab[k] = sm.red[gg][k];
+            sm.red[gg][k] = 0;
+          }
+        }
+        group_barrier(&sm.sbar, sgen, SW);  // red[] is clear for the next query
+        if (trace && qy == 0 && sw == 0 && lane == 0) trace[6] = wall_clock64();
+      }
     }
   }
-  __syncthreads();
-  for (uint32_t g = 0; g < gy; ++g) {
-    uint32_t* slab = reinterpret_cast<uint32_t*>(slabs) + ((uint64_t)g * gridDim.x + blockIdx.x) * (NQ * GW);
-    for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) slab[i] = sm.red[g][i];
-  }
-  if (trace && threadIdx.x == 0) trace[6] = wall_clock64();
 }
 
 // slabs: [grid.y][grid.x][nq][GW words]; out[a*efs + b] for b < efs.
 // One 1024-thread block per 64 output words: 16 lane groups split the gx slabs, then LDS.
+// blockIdx.y = query of a queue: slabs q_words apart, answers nq*efs bytes apart.
 __global__ __launch_bounds__(kReduceThreads) void k_reduce(const uint32_t* __restrict__ slabs,
                                                            int nq, uint32_t gw, uint32_t gx,
                                                            uint32_t pitch, uint32_t efs,
-                                                           uint8_t* __restrict__ out) {
+                                                           uint8_t* __restrict__ out,
+                                                           uint64_t q_words) {
+  slabs += blockIdx.y * q_words;
+  out += (uint64_t)blockIdx.y * nq * efs;
   __shared__ uint32_t part[kReduceThreads / 64][64];
   const uint32_t words = pitch / 4;
   const uint32_t lane = threadIdx.x & 63, grp16 = threadIdx.x >> 6, ngrp = blockDim.x >> 6;
@@ -1425,13 +1494,18 @@ hipError_t launch_fused(const TreePlan& pl, const DevKey* d_key, const NodeBufs&
 int fused_k(int tile) { return tile == 4096 ? 6 : (tile == 1024 ? 4 : 0); }
 
 // ---- single-launch query ---------------------------------------------------------------------
-QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, int num_cus) {
+QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, int num_cus,
+                          int nk) {
   QueryPlan qp{};
   const int nr = n - log_parts;
   if (nr < 0 || (uint64_t)n * (uint64_t)(p - 1) > (uint64_t)kQueryCwCap) return qp;
   const uint64_t nleaves = 1ull << nr;
-  const int tile = fused_tile(nq, pitch, nleaves, num_cus);
+  int tile = fused_tile(nq, pitch, nleaves, num_cus);
   if (!tile) return qp;
+  // a queue: 4096-leaf tiles whenever each workgroup gets at least one -- the tree of the next
+  // tile is built during the scan of the previous one, and wide tiles spend a smaller share of
+  // their tree in latency-bound narrow levels (a lone query keeps 1024: shorter first tile)
+  if (nk > 1 && nq <= 2 && nleaves >= (uint64_t)4096 * 256) tile = 4096;
   const int kt = tile == 4096 ? 12 : 10;
   int lr = 0;
   while ((2ll << lr) <= num_cus) ++lr;  // regions = largest power of two <= CUs
@@ -1446,27 +1520,30 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
 }
 
 template <int NQ, int TILE>
-static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, int p, int n, int party0,
-                           int log_parts, uint64_t prefix, const uint8_t* shard, uint8_t* slabs,
-                           hipStream_t s, uint64_t* trace) {
+static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
+                           int p, int n, int party0, int log_parts, uint64_t prefix,
+                           const uint8_t* shard, uint8_t* slabs, hipStream_t s, uint64_t* trace) {
   constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : 8));
   constexpr int VEC = NQ <= 2 ? 4 : 2;
+  constexpr int RING = TILE == 4096 ? 2 : 4;  // share slots: the tree runs RING-1 tiles ahead
   const ScanShape& sh = qp.shape;
   if (sh.uniform)
-    hipLaunchKernelGGL((k_query<NQ, NRP, VEC, true, kFusedTW, TILE, 4>), dim3(sh.grid.x),
-                       dim3(kFusedThreads), 0, s, d_raw, p, n, NQ, party0, log_parts, prefix,
-                       qp.lr, qp.lt, shard, sh.pitch, sh.cpr, sh.grid.y, slabs, trace);
+    hipLaunchKernelGGL((k_query<NQ, NRP, VEC, true, kFusedTW, TILE, 4, RING>), dim3(sh.grid.x),
+                       dim3(kFusedThreads), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,
+                       log_parts, prefix, qp.lr, qp.lt, shard, sh.pitch, sh.cpr, sh.grid.y, slabs,
+                       trace);
   else
-    hipLaunchKernelGGL((k_query<NQ, NRP, VEC, false, kFusedTW, TILE, 1>), dim3(sh.grid.x),
-                       dim3(kFusedThreads), 0, s, d_raw, p, n, NQ, party0, log_parts, prefix,
-                       qp.lr, qp.lt, shard, sh.pitch, sh.cpr, 1u, slabs, trace);
+    hipLaunchKernelGGL((k_query<NQ, NRP, VEC, false, kFusedTW, TILE, 1, RING>), dim3(sh.grid.x),
+                       dim3(kFusedThreads), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,
+                       log_parts, prefix, qp.lr, qp.lt, shard, sh.pitch, sh.cpr, 1u, slabs, trace);
   return hipGetLastError();
 }
 
-hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, int p, int n, int party0,
-                        int log_parts, uint64_t prefix, const uint8_t* shard, uint8_t* slabs,
-                        hipStream_t s, uint64_t* trace) {
-#define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, p, n, party0, log_parts, prefix, shard, slabs, s, trace)
+hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
+                        int p, int n, int party0, int log_parts, uint64_t prefix,
+                        const uint8_t* shard, uint8_t* slabs, hipStream_t s, uint64_t* trace) {
+  if (nk < 1) return hipErrorInvalidValue;
+#define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, s, trace)
   if (qp.tile == 4096) {
     switch (qp.shape.nq) {
       case 1: return PIR_Q(1, 4096);
@@ -1648,13 +1725,14 @@ hipError_t launch_scan(const ScanShape& sh, const uint8_t* d_shard, uint64_t nre
 }
 
 hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t efs,
-                         uint8_t* d_out, hipStream_t s) {
+                         uint8_t* d_out, hipStream_t s, int nk) {
   const uint32_t words = sh.pitch / 4;
   const uint32_t total = (uint32_t)sh.nq * words;
   const uint32_t gw = kColGroupLanes * sh.vec;
-  hipLaunchKernelGGL(k_reduce, dim3((total + 63) / 64), dim3(kReduceThreads), 0, s,
+  const uint64_t q_words = (uint64_t)sh.grid.x * sh.grid.y * (sh.slab_bytes / 4);
+  hipLaunchKernelGGL(k_reduce, dim3((total + 63) / 64, nk), dim3(kReduceThreads), 0, s,
                      reinterpret_cast<const uint32_t*>(d_slabs), sh.nq, gw, sh.grid.x,
-                     sh.pitch, efs, d_out);
+                     sh.pitch, efs, d_out, q_words);
   return hipGetLastError();
 }
 

@@ -171,6 +171,24 @@ class Engine:
         check(self._lib.pir_engine_answer_batch_dev(self._h, d_keys, num_keys, d_result, stream),
               "answer_batch_dev")
 
+    def answer_stream_dev(self, d_keys, num_keys, d_result, stream=None):
+        """A queue of independent queries, each its own tree and full shard pass, answered
+        back to back in one launch (device pointers; asynchronous)."""
+        check(self._lib.pir_engine_answer_stream_dev(self._h, d_keys, num_keys, d_result, stream),
+              "answer_stream_dev")
+
+    def answer_stream(self, keys):
+        """Host form of answer_stream_dev: [num_keys, num_rounds, record_bytes]."""
+        keys = [bytes(k) for k in keys]
+        nk = len(keys)
+        d_k = self.alloc_dev(max(1, nk * self.key_len))
+        d_r = self.alloc_dev(max(1, nk * self.answer_bytes))
+        if nk:
+            self.h2d(d_k, b"".join(keys))
+        self.answer_stream_dev(d_k, nk, d_r)
+        self.sync()
+        return self.d2h(d_r, nk * self.answer_bytes).reshape(nk, self.num_rounds, self.record_bytes)
+
     @property
     def stream(self):
         return self._lib.pir_engine_stream(self._h)
@@ -200,12 +218,15 @@ class Engine:
     TRACE_PHASES = ["start", "key_parsed", "first_tile_root", "tile0_ready", "last_tile_ready",
                     "scan_done", "end"]
 
-    def trace_query(self, d_key):
-        """One single-launch answer with per-workgroup phase stamps (diagnostics): an array
-        [workgroups, 64] of microseconds since the earliest workgroup start (layout:
-        pir_engine_trace_query in include/pir_engine.h; 0 = stamp not reached)."""
-        out = np.zeros((4096, 64), np.uint64)
-        n = self._lib.pir_engine_trace_query(self._h, d_key, out.ctypes.data_as(ctypes.c_void_p), 4096)
+    def trace_query(self, d_key, num_keys=1):
+        """One single-launch answer of a queue of num_keys keys (at d_key, key_len apart) with
+        per-workgroup phase stamps (diagnostics): an array [workgroups, 160] of microseconds
+        since the earliest workgroup start (layout: pir_engine_trace_query in
+        include/pir_engine.h; 0 = stamp not reached; columns 56-57 and 128+ are raw shader-clock
+        ticks, divided by 100 like the rest)."""
+        out = np.zeros((4096, 160), np.uint64)
+        n = self._lib.pir_engine_trace_query(self._h, d_key, num_keys,
+                                             out.ctypes.data_as(ctypes.c_void_p), 4096)
         check(min(n, 0), "trace_query")
         return out[:n].astype(np.float64) / 100.0
 

@@ -94,6 +94,12 @@ int pir_engine_answer_batch_dev(pir_engine_t *e, const uint8_t *d_keys, int num_
 /* host-buffer form of the above (synchronous) */
 int pir_engine_answer_batch(pir_engine_t *e, const uint8_t *keys, int num_keys,
                             uint8_t *results);
+/* a queue of `num_keys` independent queries (keys of key_len bytes back to back; results
+ * num_keys x num_rounds x record_bytes), each answered exactly as pir_engine_answer_dev would
+ * -- its own DPF tree and its own full pass over the shard -- back to back in one launch where
+ * the shape allows, so that the tree of query k+1 is built while query k's rows stream. */
+int pir_engine_answer_stream_dev(pir_engine_t *e, const uint8_t *d_keys, int num_keys,
+                                 uint8_t *d_result, void *stream);
 /* keys per shard pass: 0 = automatic (8 / nrp), else a power of two <= 16 / nrp, where nrp =
  * num_rounds rounded up to a power of two.  Default from $PIR_BATCH_G. */
 int pir_engine_set_batch_group(pir_engine_t *e, int keys_per_pass);
@@ -119,13 +125,17 @@ int pir_engine_last_timings(pir_engine_t *e, pir_kernel_time *out, int max);
  * mean ms of key_prep, tree_frontier, tree_stages (all expand stages), scan (one launch over
  * all rows), reduce.  d_key: device pointer to one raw key. */
 int pir_engine_profile_phases(pir_engine_t *e, const uint8_t *d_key, int iters, float *out_ms);
-/* diagnostics: one single-launch answer (k_query) with per-workgroup phase stamps.  out holds
- * max_wgs x 64 uint64 wall-clock ticks (100 MHz) relative to the earliest start (0 = not
- * reached): [0..6] start, key parsed, first tile root, tile 0 shares ready, last tile ready,
- * scan done, end; [8+d] descent level d of the first tile root (d < 32); [40+l] expansion level
- * l of tile 0 (l < 16).  Returns the number of workgroups (>= 0), or an error code;
- * PIR_EINVAL when the shape does not use k_query. */
-int pir_engine_trace_query(pir_engine_t *e, const uint8_t *d_key, uint64_t *out, int max_wgs);
+/* diagnostics: one single-launch answer (k_query) of a queue of num_keys keys with
+ * per-workgroup phase stamps.  out holds max_wgs x 128 uint64 wall-clock ticks (100 MHz)
+ * relative to the earliest start (0 = not reached): [0..6] start, key parsed, first tile root,
+ * tile 0 shares ready, last tile of query 0 ready, query 0 scanned, query 0 slab written;
+ * [8+d] descent level d of the first tile root (d < 32); [40+l] expansion level l of tile 0
+ * (l < 16); [56], [57] shader clock (s_memtime) at start and at the first tile root; [64+g]
+ * queue tile g ready, [96+g] queue tile g consumed by scan wave 0, [128+g] shader clock at
+ * [64+g] (g < 32).  Returns the number
+ * of workgroups (>= 0), or an error code; PIR_EINVAL when the shape does not use k_query. */
+int pir_engine_trace_query(pir_engine_t *e, const uint8_t *d_key, int num_keys, uint64_t *out,
+                           int max_wgs);
 
 /* ---- split shard across GPUs: XOR all-reduce of partition answers over RCCL ---- */
 #define PIR_COMM_ID_BYTES 128

@@ -38,7 +38,7 @@ __global__ __launch_bounds__(1024) void k_col(int iters, uint32_t* out, long lon
 }
 
 template <int NB, int LASTW>
-__global__ __launch_bounds__(64) void k_row(int iters, uint32_t* out, long long* cyc) {
+__global__ __launch_bounds__(1024) void k_row(int iters, uint32_t* out, long long* cyc) {
   __shared__ uint32_t tab[2 * 256 * 32];
   load_tables(tab);
   __syncthreads();
@@ -52,8 +52,8 @@ __global__ __launch_bounds__(64) void k_row(int iters, uint32_t* out, long long*
     if (NB > 1) s.x ^= o[NB - 1].x & 1u;
   }
   const long long t1 = clock64();
-  out[threadIdx.x] = s.x ^ s.y ^ s.z ^ s.w;
-  if (threadIdx.x == 0) *cyc = t1 - t0;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s.x ^ s.y ^ s.z ^ s.w;
+  if (threadIdx.x == 0 && blockIdx.x == 0) *cyc = t1 - t0;
 }
 
 static uint32_t* g_o;
@@ -82,7 +82,7 @@ static void run(const char* name, void (*launch)()) {
 
 int main() {
   upload_te0(nullptr);
-  (void)hipMalloc(&g_o, 256 * 64 * 4);
+  (void)hipMalloc(&g_o, 256 * 1024 * 4);
   (void)hipMalloc(&g_c, 8);
   run("col", [] { hipLaunchKernelGGL(k_col, dim3(1), dim3(64), 0, 0, kIters, g_o, g_c); });
   run("col256", [] { hipLaunchKernelGGL(k_col, dim3(256), dim3(64), 0, 0, kIters, g_o, g_c); });
@@ -90,5 +90,14 @@ int main() {
   run("colWG256", [] { hipLaunchKernelGGL(k_col, dim3(256), dim3(1024), 0, 0, kIters, g_o, g_c); });
   run("row3", [] { hipLaunchKernelGGL((k_row<3, 1>), dim3(1), dim3(64), 0, 0, kIters, g_o, g_c); });
   run("row1", [] { hipLaunchKernelGGL((k_row<1, 4>), dim3(1), dim3(64), 0, 0, kIters, g_o, g_c); });
+  // throughput: 256 CUs x W waves of row3 / row1 (blocks per second chip-wide)
+  for (int w : {4, 8, 16}) {
+    static int ws;
+    ws = w;
+    printf("row3 x %2d waves/CU: ", w);
+    run("", [] { hipLaunchKernelGGL((k_row<3, 1>), dim3(256), dim3(64 * ws), 0, 0, kIters, g_o, g_c); });
+    printf("row1 x %2d waves/CU: ", w);
+    run("", [] { hipLaunchKernelGGL((k_row<1, 4>), dim3(256), dim3(64 * ws), 0, 0, kIters, g_o, g_c); });
+  }
   return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }

@@ -21,17 +21,19 @@ def main():
     ap.add_argument("--p", type=int, default=2)
     ap.add_argument("--nq", type=int, default=1)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--queue", type=int, default=1, help="keys in the traced queue")
     a = ap.parse_args()
     import erasurecodedpir_amd as pir
     e = pir.Engine(a.p, 1, a.n, a.efs, a.nq)
     e.fill_shard_random(1)
-    keys = pir.gen_keys(a.n, (1 << a.n) // 3, a.p, a.nq)
-    d_key = e.alloc_dev(e.key_len)
-    e.h2d(d_key, keys[0])
+    keys = [pir.gen_keys(a.n, (1 << a.n) // 3 + 17 * k, a.p, a.nq) for k in range(a.queue)]
+    d_key = e.alloc_dev(e.key_len * a.queue)
+    e.h2d(d_key, b"".join(k[0] for k in keys))
+    keys = keys[0]
     for _ in range(3):
         e.answer(keys[0])
     for r in range(a.reps):
-        tr = e.trace_query(d_key)
+        tr = e.trace_query(d_key, a.queue)
         print(f"n={a.n} efs={a.efs} p={a.p} nq={a.nq}: {tr.shape[0]} workgroups (rep {r})")
         for i, name in enumerate(e.TRACE_PHASES):
             col = tr[:, i]
@@ -44,6 +46,14 @@ def main():
         raw = tr * 100.0  # back to ticks for the clock columns
         ghz = (raw[:, 57] - raw[:, 56]) / ((tr[:, 2] - tr[:, 0]) * 1e3)
         print(f"  shader clock start->first root: med {np.median(ghz):.3f} GHz (min {ghz.min():.3f} max {ghz.max():.3f})")
+        if a.queue > 1:
+            rd = [med[64 + g] for g in range(32) if tr[:, 64 + g].all()]
+            cs = [med[96 + g] for g in range(32) if tr[:, 96 + g].all()]
+            print("  queue tile ready    (med us):", " ".join(f"{v:.0f}" for v in rd))
+            print("  queue tile consumed (med us):", " ".join(f"{v:.0f}" for v in cs))
+            ck = [(tr[:, 128 + g + 1] - tr[:, 128 + g]) * 100 / ((tr[:, 64 + g + 1] - tr[:, 64 + g]) * 1e3)
+                  for g in range(len(rd) - 1)]
+            print("  shader clock between ready stamps (GHz):", " ".join(f"{np.median(c):.2f}" for c in ck))
     e.close()
 
 
