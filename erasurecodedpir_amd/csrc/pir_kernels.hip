@@ -601,6 +601,11 @@ __device__ __forceinline__ void lds_wait_geq(const uint32_t* p, uint32_t v) {
   while (lds_load(p) < v) __builtin_amdgcn_s_sleep(1);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
+// the same for a wait expected to be long (a tree wave far ahead of the scan): polls ~0.5 us apart
+__device__ __forceinline__ void lds_wait_geq_idle(const uint32_t* p, uint32_t v) {
+  while (lds_load(p) < v) __builtin_amdgcn_s_sleep(16);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 __device__ __forceinline__ void lds_signal(uint32_t* p) {  // one lane per wave
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if ((threadIdx.x & 63) == 0)
@@ -1147,7 +1152,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
     // ===================================== tree role ======================================
     for (uint32_t g = 1; g < total; ++g) {
       // slot g % RING free: every scan wave has consumed tile g - RING (per-slot counts)
-      if (g >= (uint32_t)RING) lds_wait_geq(&sm.consumed[g % RING], (g / RING) * SW);
+      if (g >= (uint32_t)RING) lds_wait_geq_idle(&sm.consumed[g % RING], (g / RING) * SW);
       tree_tile(g, TW * 64, TW);
     }
   } else {
