@@ -108,6 +108,9 @@ PROTOTYPES = {
     "initialize_client": (None, [ctypes.POINTER(CClient), ctypes.c_uint8, _U32]),
     "free_client": (None, [ctypes.POINTER(CClient)]),
     "encode_across_files_server": (None, [ctypes.POINTER(CClient), ctypes.POINTER(CServer)]),
+    "assembleDPFTreeQueryResponses": (None, [ctypes.POINTER(CClient), _P,
+                                             ctypes.POINTER(ctypes.POINTER(c_u8_p)), _P]),
+    "lagrangeInterpolationSemihonest": (None, [_P, ctypes.c_uint8, _P, ctypes.c_uint8, _P]),
     "pirSetDevice": (None, [_I]),
     "pirServerShardChanged": (None, [ctypes.POINTER(CServer)]),
 }

@@ -992,7 +992,7 @@ int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, int num_keys, 
   for (int w = 0; w < n; ++w)
     for (int k = 0; k < pir::kQueryTraceSlots; ++k) {
       const uint64_t v = h[(size_t)w * pir::kQueryTraceSlots + k];
-      const bool clk = k == 56 || k == 57 || k >= 128;  // shader-clock ticks, not wall time
+      const bool clk = k == 56 || k == 57 || (k >= 128 && k < 160);  // shader-clock ticks
       out[(size_t)w * pir::kQueryTraceSlots + k] = clk ? v : (v ? v - t0 : 0);
     }
   return nwg;

@@ -111,6 +111,7 @@ hipError_t launch_fused(const TreePlan& pl, const DevKey* d_key, const NodeBufs&
 // tile == 0: shape not supported.
 struct QueryPlan {
   int tile, lr, lt;
+  int tw;           // tree waves per workgroup (the rest scan)
   ScanShape shape;  // grid.x = 2^lr workgroups (slabs), grid.y = column groups
 };
 QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, int num_cus,
@@ -118,7 +119,7 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
 inline size_t query_slab_bytes(const QueryPlan& qp) {
   return (size_t)qp.shape.grid.x * qp.shape.grid.y * qp.shape.slab_bytes;
 }
-constexpr int kQueryTraceSlots = 160;  // trace: per-workgroup phase stamps (wall clock, 100 MHz)
+constexpr int kQueryTraceSlots = 192;  // trace: per-workgroup phase stamps (wall clock, 100 MHz)
 hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
                         int p, int n, int party0, int log_parts, uint64_t prefix,
                         const uint8_t* shard, uint8_t* slabs, hipStream_t s,

@@ -18,6 +18,7 @@
 #include "pir_aes.h"
 
 #include <algorithm>
+#include <stdlib.h>
 
 namespace pir {
 
@@ -1022,6 +1023,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
       if (trace && g == 0 && lane == 0) { trace[2] = wall_clock64(); trace[57] = clock64(); }
     }
     sync();
+    if (trace && g == 1 && tt == 0) trace[176] = wall_clock64();
     // ---- breadth-first expansion of the tile root ------------------------------------------
     // level i of a tile (width 2^i) lives in buffer a when (KT-1-i) is even, else b
     int buf = (KT - 1) & 1;
@@ -1082,6 +1084,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
       }
       sync();
       if (trace && g == 0 && tt == 0 && lv < 16) trace[40 + lv] = wall_clock64();
+      if (trace && g == 1 && tt == 0 && lv < 16) trace[160 + lv] = wall_clock64();
       buf ^= 1;
       W *= 2;
     }
@@ -1423,6 +1426,7 @@ TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last) {
 
 // ---- fused leaf stage + scan -----------------------------------------------------------------
 constexpr int kFusedTW = 8;       // tree waves per workgroup (the other 8 scan)
+constexpr int kQueryTreeHeavyTW = 12;  // k_query for small records: 12 tree + 4 scan waves
 constexpr int kFusedTileIn = 64;  // tree nodes entering a tile
 
 int fused_tile(int nq, uint32_t pitch, uint64_t nleaves, int num_cus) {
@@ -1511,6 +1515,13 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
   // tile is built during the scan of the previous one, and wide tiles spend a smaller share of
   // their tree in latency-bound narrow levels (a lone query keeps 1024: shorter first tile)
   if (nk > 1 && nq <= 2 && nleaves >= (uint64_t)4096 * 256) tile = 4096;
+  // records of <= 256 B: a tile's rows stream in a quarter of the time its tree takes, so 12 of
+  // the 16 waves build trees and 4 scan ($PIR_QUERY_TW = 8 or 12 overrides)
+  qp.tw = (nq <= 2 && pitch <= 256) ? kQueryTreeHeavyTW : kFusedTW;
+  if (const char* tw = getenv("PIR_QUERY_TW")) {
+    const int v = atoi(tw);
+    if (v == kFusedTW || (v == kQueryTreeHeavyTW && nq <= 2)) qp.tw = v;
+  }
   const int kt = tile == 4096 ? 12 : 10;
   int lr = 0;
   while ((2ll << lr) <= num_cus) ++lr;  // regions = largest power of two <= CUs
@@ -1532,15 +1543,20 @@ static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t k
   constexpr int VEC = NQ <= 2 ? 4 : 2;
   constexpr int RING = TILE == 4096 ? 2 : 4;  // share slots: the tree runs RING-1 tiles ahead
   const ScanShape& sh = qp.shape;
-  if (sh.uniform)
-    hipLaunchKernelGGL((k_query<NQ, NRP, VEC, true, kFusedTW, TILE, 4, RING>), dim3(sh.grid.x),
-                       dim3(kFusedThreads), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,
-                       log_parts, prefix, qp.lr, qp.lt, shard, sh.pitch, sh.cpr, sh.grid.y, slabs,
-                       trace);
-  else
-    hipLaunchKernelGGL((k_query<NQ, NRP, VEC, false, kFusedTW, TILE, 1, RING>), dim3(sh.grid.x),
-                       dim3(kFusedThreads), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,
-                       log_parts, prefix, qp.lr, qp.lt, shard, sh.pitch, sh.cpr, 1u, slabs, trace);
+#define PIR_QL(UNI, TW, GY, gy)                                                                  \
+  hipLaunchKernelGGL((k_query<NQ, NRP, VEC, UNI, TW, TILE, GY, RING>), dim3(sh.grid.x),          \
+                     dim3(kFusedThreads), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,          \
+                     log_parts, prefix, qp.lr, qp.lt, shard, sh.pitch, sh.cpr, gy, slabs, trace)
+  if constexpr (NQ <= 2) {
+    if (qp.tw == kQueryTreeHeavyTW) {  // small records: the tree is the bottleneck
+      if (sh.uniform) PIR_QL(true, kQueryTreeHeavyTW, 4, sh.grid.y);
+      else PIR_QL(false, kQueryTreeHeavyTW, 1, 1u);
+      return hipGetLastError();
+    }
+  }
+  if (sh.uniform) PIR_QL(true, kFusedTW, 4, sh.grid.y);
+  else PIR_QL(false, kFusedTW, 1, 1u);
+#undef PIR_QL
   return hipGetLastError();
 }
 

@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <utility>
 #include <vector>
 
 #include "../../include/pir_engine.h"
@@ -126,9 +127,129 @@ uint8_t gf_pow_h(uint8_t base, int exp) {  // coding.cpp:46-60 (pow(0, e) == 1 t
   return r;
 }
 
+uint8_t gf_inv_h(uint8_t a) {  // a^254 (coding.cpp:24-33: inv(0) == 0)
+  if (!a) return 0;
+  uint8_t r = 1, b = a;
+  for (int e = 254; e; e >>= 1) {
+    if (e & 1) r = gf_mul_h(r, b);
+    b = gf_mul_h(b, b);
+  }
+  return r;
+}
+
+// Gauss-Jordan over GF(2^8) (coding.cpp:73-126): out = in^-1; false if singular; `in` destroyed
+bool gf_invert_matrix_h(std::vector<uint8_t>& in, std::vector<uint8_t>& out, int n) {
+  out.assign((size_t)n * n, 0);
+  for (int i = 0; i < n; ++i) out[(size_t)i * n + i] = 1;
+  for (int i = 0; i < n; ++i) {
+    if (!in[(size_t)i * n + i]) {  // swap in a row with a non-zero pivot
+      int j = i + 1;
+      while (j < n && !in[(size_t)j * n + i]) ++j;
+      if (j == n) return false;
+      for (int k = 0; k < n; ++k) {
+        std::swap(in[(size_t)i * n + k], in[(size_t)j * n + k]);
+        std::swap(out[(size_t)i * n + k], out[(size_t)j * n + k]);
+      }
+    }
+    const uint8_t piv = gf_inv_h(in[(size_t)i * n + i]);
+    for (int k = 0; k < n; ++k) {
+      in[(size_t)i * n + k] = gf_mul_h(in[(size_t)i * n + k], piv);
+      out[(size_t)i * n + k] = gf_mul_h(out[(size_t)i * n + k], piv);
+    }
+    for (int j = 0; j < n; ++j) {
+      if (j == i) continue;
+      const uint8_t x = in[(size_t)j * n + i];
+      if (!x) continue;
+      for (int k = 0; k < n; ++k) {
+        out[(size_t)j * n + k] ^= gf_mul_h(x, out[(size_t)i * n + k]);
+        in[(size_t)j * n + k] ^= gf_mul_h(x, in[(size_t)i * n + k]);
+      }
+    }
+  }
+  return true;
+}
+
+// Inverse of the Vandermonde system of interpolation.cpp:176-196 on the first m = deg+1 points:
+// gen[i][c] = pts[i]^c (calcFuncCoeffs, interpolation.cpp:50-54)
+std::vector<uint8_t> vandermonde_inverse(const uint8_t* pts, int m) {
+  std::vector<uint8_t> gen((size_t)m * m), inv;
+  for (int i = 0; i < m; ++i)
+    for (int c = 0; c < m; ++c) gen[(size_t)i * m + c] = gf_pow_h(pts[i], c);
+  if (!gf_invert_matrix_h(gen, inv, m)) {
+    fprintf(stderr, "pir shim: singular interpolation system (repeated evaluation points)\n");
+    abort();
+  }
+  return inv;
+}
+
 }  // namespace
 
 extern "C" {
+
+// interpolation.cpp:176-196: coefficients of the degree-funcDegree polynomial through the first
+// funcDegree+1 (evalPoints[i], evals[i]); output[c] = coefficient of x^c
+void lagrangeInterpolationSemihonest(uint8_t* evalPoints, uint8_t numPoints, uint8_t* evals,
+                                     uint8_t funcDegree, uint8_t* output) {
+  const int m = funcDegree + 1;
+  if (numPoints < m) {  // the reference asserts (interpolation.cpp:179)
+    fprintf(stderr, "pir shim: %d points for a degree-%d interpolation\n", numPoints, funcDegree);
+    abort();
+  }
+  const std::vector<uint8_t> inv = vandermonde_inverse(evalPoints, m);
+  for (int i = 0; i < m; ++i) {  // computeMatrixTimesResponse (interpolation.cpp:40-48)
+    uint8_t v = 0;
+    for (int j = 0; j < m; ++j) v ^= gf_mul_h(evals[j], inv[(size_t)i * m + j]);
+    output[i] = v;
+  }
+}
+
+// client.cpp:211-268 (semi-honest, B == 0): responses[j][round][byte] from the NUM_PARTIES - R
+// servers not erased (erasureIndexList[q-1] == 1 for server q, in increasing q), output =
+// FILE_SIZE_BYTES of the record.  Round i peels the coefficients recovered in rounds < i off
+// the shares, then interpolates each byte position; the evaluation points are the same for
+// every byte, so the Vandermonde system is inverted once per round, not once per byte.
+void assembleDPFTreeQueryResponses(client* c, uint8_t* erasureIndexList, uint8_t*** responses,
+                                   uint8_t* output) {
+  (void)c;
+  if (B > 0) {
+    fprintf(stderr, "pir shim: malicious (B > 0) decoding is outside the engine's scope\n");
+    abort();
+  }
+  const int nr = NUM_PARTIES - R, efs = ENCODED_FILE_SIZE_BYTES, m = K + RHO;
+  if (nr < m) {
+    fprintf(stderr, "pir shim: %d responses cannot decode degree %d\n", nr, m - 1);
+    abort();
+  }
+  std::vector<uint8_t> acc((size_t)K * efs, 0), pts(nr), sh((size_t)nr);
+  for (int i = 0; i < NUM_ROUNDS; ++i) {
+    int cur = 1;
+    for (int j = 0; j < nr; ++j) {
+      while (!erasureIndexList[cur - 1]) ++cur;
+      pts[j] = (uint8_t)cur++;
+    }
+    const std::vector<uint8_t> inv = vandermonde_inverse(pts.data(), m);
+    std::vector<uint8_t> peel((size_t)nr * i);  // gf_pow(point_j, K + i - b), b < i
+    for (int j = 0; j < nr; ++j)
+      for (int b = 0; b < i; ++b) peel[(size_t)j * i + b] = gf_pow_h(pts[j], K + i - b);
+    for (int a = 0; a < efs; ++a) {
+      for (int j = 0; j < nr; ++j) {
+        uint8_t v = responses[j][i][a];
+        for (int b = 0; b < i; ++b)
+          v ^= gf_mul_h(acc[(size_t)(K - 1 - b) * efs + a], peel[(size_t)j * i + b]);
+        sh[j] = v;
+      }
+      for (int q = 0; q < RHO; ++q) {  // coefficient K+RHO-1-q of the interpolant
+        const int row = m - 1 - q;
+        uint8_t v = 0;
+        for (int j = 0; j < m; ++j) v ^= gf_mul_h(sh[j], inv[(size_t)row * m + j]);
+        const int dst = K - 1 - i - q;
+        if (dst >= 0) acc[(size_t)dst * efs + a] = v;
+      }
+    }
+  }
+  memcpy(output, acc.data(), FILE_SIZE_BYTES);
+}
+
 
 void pirSetDevice(int device) { g_device = device; }
 

@@ -220,11 +220,11 @@ class Engine:
 
     def trace_query(self, d_key, num_keys=1):
         """One single-launch answer of a queue of num_keys keys (at d_key, key_len apart) with
-        per-workgroup phase stamps (diagnostics): an array [workgroups, 160] of microseconds
+        per-workgroup phase stamps (diagnostics): an array [workgroups, 192] of microseconds
         since the earliest workgroup start (layout: pir_engine_trace_query in
-        include/pir_engine.h; 0 = stamp not reached; columns 56-57 and 128+ are raw shader-clock
+        include/pir_engine.h; 0 = stamp not reached; columns 56-57 and 128-159 are raw shader-clock
         ticks, divided by 100 like the rest)."""
-        out = np.zeros((4096, 160), np.uint64)
+        out = np.zeros((4096, 192), np.uint64)
         n = self._lib.pir_engine_trace_query(self._h, d_key, num_keys,
                                              out.ctypes.data_as(ctypes.c_void_p), 4096)
         check(min(n, 0), "trace_query")

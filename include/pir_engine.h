@@ -132,7 +132,8 @@ int pir_engine_profile_phases(pir_engine_t *e, const uint8_t *d_key, int iters, 
  * [8+d] descent level d of the first tile root (d < 32); [40+l] expansion level l of tile 0
  * (l < 16); [56], [57] shader clock (s_memtime) at start and at the first tile root; [64+g]
  * queue tile g ready, [96+g] queue tile g consumed by scan wave 0, [128+g] shader clock at
- * [64+g] (g < 32).  Returns the number
+ * [64+g] (g < 32); [160+l] expansion level l of queue tile 1 (built by the tree waves beside
+ * the scan), [176] its root ready.  Returns the number
  * of workgroups (>= 0), or an error code; PIR_EINVAL when the shape does not use k_query. */
 int pir_engine_trace_query(pir_engine_t *e, const uint8_t *d_key, int num_keys, uint64_t *out,
                            int max_wgs);

@@ -16,6 +16,8 @@
  *   client / initialize_client / free_client / encode_across_files_server
  *                                      client.h:15-28,  client.cpp:16-41, :70-97 (server setup
  *                                      path of src/server/server.go:299-331)
+ *   assembleDPFTreeQueryResponses      client.h:33,     client.cpp:211-268 (client decode)
+ *   lagrangeInterpolationSemihonest    interpolation.h:10, interpolation.cpp:176-196
  *   calcOptimizedDPFTreeKeyLength      utils.h:26,      utils.cpp:85-90
  *
  * Deliberate differences (each a reference defect):
@@ -86,6 +88,14 @@ void assemblDPFTreeQueryThreadResults(server *s, uint8_t ***in, int numThreads, 
 void initialize_client(client *c, uint8_t log_num_files, uint32_t file_size_bytes);
 void free_client(client *c);
 void encode_across_files_server(client *c, server *s);
+/* client-side erasure decode of one tree-mode query (client.h:33, client.cpp:211-268,
+ * semi-honest: B == 0): responses[j][round][byte] from the NUM_PARTIES - R servers q with
+ * erasureIndexList[q-1] == 1, in increasing q; output = the FILE_SIZE_BYTES record. */
+void assembleDPFTreeQueryResponses(client *c, uint8_t *erasureIndexList, uint8_t ***responses,
+                                   uint8_t *output);
+/* interpolation.h:10, interpolation.cpp:176-196 */
+void lagrangeInterpolationSemihonest(uint8_t *evalPoints, uint8_t numPoints, uint8_t *evals,
+                                     uint8_t funcDegree, uint8_t *output);
 
 /* Engine device used by servers created after this call (default: $PIR_DEVICE or 0). */
 void pirSetDevice(int device);

@@ -54,6 +54,9 @@ def main():
             ck = [(tr[:, 128 + g + 1] - tr[:, 128 + g]) * 100 / ((tr[:, 64 + g + 1] - tr[:, 64 + g]) * 1e3)
                   for g in range(len(rd) - 1)]
             print("  shader clock between ready stamps (GHz):", " ".join(f"{np.median(c):.2f}" for c in ck))
+            t1 = [med[176]] + [med[160 + k] for k in range(16) if tr[:, 160 + k].all()]
+            print("  tile-1 root + level ends (med us, tree waves beside the scan):",
+                  " ".join(f"{v:.1f}" for v in t1), f"| ready {med[65]:.1f}")
     e.close()
 
 
