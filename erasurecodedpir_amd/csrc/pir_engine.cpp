@@ -721,6 +721,25 @@ int pir_engine_fill_shard_random(pir_engine_t* e, uint64_t seed) {
   return PIR_OK;
 }
 
+int pir_engine_encode_across_dev(pir_engine_t* e, const uint8_t* d_files, uint64_t file_pitch,
+                                 uint64_t num_files, int k) {
+  if (!e) return fail(PIR_EINVAL, "null engine");
+  if (k < 1 || k > 16) return fail(PIR_EINVAL, "k = %d outside [1,16]", k);
+  if (d_files && file_pitch < e->cfg.record_bytes) return fail(PIR_EINVAL, "file_pitch < record_bytes");
+  const uint64_t encdb = (num_files + (uint64_t)k - 1) / (uint64_t)k;
+  if (encdb > (1ull << e->cfg.log_num_records))
+    return fail(PIR_EINVAL, "%llu files over k=%d need %llu rows > 2^%d", (unsigned long long)num_files,
+                k, (unsigned long long)encdb, e->cfg.log_num_records);
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const uint64_t row0 = (uint64_t)e->cfg.partition_index * e->rows;
+  HIP_TRY(pir::launch_encode_across(d_files, file_pitch, num_files, k, e->cfg.party_index,
+                                    e->d_shard, e->rows, row0, e->pitch, e->cfg.record_bytes,
+                                    e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return PIR_OK;
+}
+
 int pir_engine_get_shard_row(pir_engine_t* e, uint64_t row, uint8_t* out) {
   if (!e || !out) return fail(PIR_EINVAL, "null argument");
   if (row >= e->rows) return fail(PIR_EINVAL, "row %llu beyond shard", (unsigned long long)row);

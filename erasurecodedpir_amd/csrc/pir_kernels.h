@@ -132,6 +132,12 @@ hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t e
 hipError_t launch_xor_fold(const uint8_t* d_in, int nranks, size_t len, uint8_t* d_out,
                            hipStream_t s);
 hipError_t launch_fill_random(uint8_t* d, size_t bytes, uint64_t seed, hipStream_t s);
+// the erasure-coded shard of server `party` (client.cpp:70-97): rows [row0, row0+rows) of the
+// global encoded database from nfiles files (d_files rows file_pitch apart, or nullptr: the
+// reference's synthetic database, client.cpp:16-33)
+hipError_t launch_encode_across(const uint8_t* d_files, uint64_t file_pitch, uint64_t nfiles,
+                               int k, int party, uint8_t* d_shard, uint64_t rows, uint64_t row0,
+                               uint32_t pitch, uint32_t efs, hipStream_t s);
 hipError_t launch_fill_shard(uint8_t* d_shard, uint64_t rows, uint32_t pitch, uint32_t efs,
                              uint64_t global_row0, uint64_t seed, hipStream_t s);
 

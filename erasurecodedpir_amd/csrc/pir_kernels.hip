@@ -1376,6 +1376,77 @@ __global__ void k_fill_shard(uint8_t* __restrict__ shard, uint64_t rows, uint32_
 }
 
 // ------------------------------------------------------------------------------------------
+// k_encode_across: the server's erasure-coded shard (client.cpp:70-97, every row of
+// generate_encoded_across_file): row r of party q = XOR_{j<k, src = encdb*j + r < nfiles}
+// gf_pow(q, j) * file[src] over GF(2^8)/0x11d.  One lane per 16-byte chunk of a row; the k
+// coefficients are wave-uniform (scalar branches over their bits, x * alpha^b by xtime).
+// files == nullptr: the reference's synthetic database (client.cpp:16-33): file v holds the
+// byte (v & 0xff) in every position, file 1 holds 0, 1, 2, ....
+// ------------------------------------------------------------------------------------------
+struct EncodeCoefs {
+  uint8_t c[16];
+};
+
+__device__ __forceinline__ uint4 gf_mul_const4(uint4 x, uint32_t c) {
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  for (int b = 0; b < 8; ++b) {
+    if (c & (1u << b)) acc = xor4(acc, x);
+    x = make_uint4(gf_xtime4(x.x), gf_xtime4(x.y), gf_xtime4(x.z), gf_xtime4(x.w));
+  }
+  return acc;
+}
+
+__device__ __forceinline__ uint32_t synth_word(uint64_t v, uint32_t b0) {  // bytes b0..b0+3
+  if (v == 1) {
+    uint32_t w = 0;
+    for (int t = 0; t < 4; ++t) w |= ((b0 + t) & 0xffu) << (8 * t);
+    return w;
+  }
+  return (uint32_t)(v & 0xff) * 0x01010101u;
+}
+
+__global__ void k_encode_across(const uint8_t* __restrict__ files, uint64_t fpitch,
+                                uint64_t nfiles, uint64_t encdb, int k, EncodeCoefs co,
+                                uint8_t* __restrict__ shard, uint64_t rows, uint64_t row0,
+                                uint32_t pitch, uint32_t efs) {
+  const uint32_t cpr = pitch / 16;
+  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * cpr) return;
+  const uint64_t r = idx / cpr;
+  const uint32_t ch = (uint32_t)(idx - r * cpr);
+  const uint64_t gr = row0 + r;
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  for (int j = 0; j < k; ++j) {
+    const uint64_t src = encdb * (uint64_t)j + gr;
+    if (src >= nfiles) continue;
+    uint4 x;
+    if (files && (fpitch & 15u) == 0 && ch * 16u + 16u <= efs) {  // aligned whole chunk
+      x = *reinterpret_cast<const uint4*>(files + src * fpitch + ch * 16u);
+    } else if (files) {
+      uint32_t w[4];
+      const uint8_t* f = files + src * fpitch + ch * 16u;
+      for (int t = 0; t < 4; ++t) {
+        uint32_t v = 0;
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t bi = ch * 16u + 4u * t + u;
+          if (bi < efs) v |= (uint32_t)f[4 * t + u] << (8 * u);
+        }
+        w[t] = v;
+      }
+      x = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      x = make_uint4(synth_word(src, ch * 16u), synth_word(src, ch * 16u + 4),
+                     synth_word(src, ch * 16u + 8), synth_word(src, ch * 16u + 12));
+    }
+    acc = xor4(acc, gf_mul_const4(x, co.c[j]));
+  }
+  uint32_t w[4] = {acc.x, acc.y, acc.z, acc.w};
+  for (int t = 0; t < 16; ++t)
+    if (ch * 16u + t >= efs) w[t >> 2] &= ~(0xffu << (8 * (t & 3)));  // zero pad bytes
+  *reinterpret_cast<uint4*>(shard + r * pitch + ch * 16u) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// ------------------------------------------------------------------------------------------
 // host side: tables, plans, launchers
 // ------------------------------------------------------------------------------------------
 TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last) {
@@ -1767,6 +1838,31 @@ hipError_t launch_xor_fold(const uint8_t* d_in, int nranks, size_t len, uint8_t*
 hipError_t launch_fill_random(uint8_t* d, size_t bytes, uint64_t seed, hipStream_t s) {
   hipLaunchKernelGGL(k_fill_random, dim3((unsigned)((bytes + 255) / 256)), dim3(256), 0, s, d,
                      bytes, seed);
+  return hipGetLastError();
+}
+
+hipError_t launch_encode_across(const uint8_t* d_files, uint64_t file_pitch, uint64_t nfiles,
+                               int k, int party, uint8_t* d_shard, uint64_t rows, uint64_t row0,
+                               uint32_t pitch, uint32_t efs, hipStream_t s) {
+  if (k < 1 || k > 16) return hipErrorInvalidValue;
+  EncodeCoefs co{};
+  for (int j = 0; j < k; ++j) {  // gf_pow(party, j) (coding.cpp:46-60; pow(0, e) == 1)
+    uint32_t r = 1;
+    for (int t = 0; t < j && party; ++t) {
+      uint32_t a = r, b = (uint32_t)party, m = 0;
+      while (b) {
+        if (b & 1) m ^= a;
+        a = ((a << 1) ^ ((a & 0x80) ? 0x11d : 0)) & 0xff;
+        b >>= 1;
+      }
+      r = m;
+    }
+    co.c[j] = (uint8_t)r;
+  }
+  const uint64_t encdb = (nfiles + k - 1) / k;
+  const uint64_t total = rows * (pitch / 16);
+  hipLaunchKernelGGL(k_encode_across, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                     d_files, file_pitch, nfiles, encdb, k, co, d_shard, rows, row0, pitch, efs);
   return hipGetLastError();
 }
 

@@ -78,6 +78,19 @@ class Engine:
     def fill_shard_random(self, seed):
         check(self._lib.pir_engine_fill_shard_random(self._h, seed), "fill_shard_random")
 
+    def encode_across(self, num_files, k, files=None):
+        """The erasure-coded shard computed on the GPU (client.cpp:70-97): from `files`
+        (num_files x record_bytes host array) or, files=None, the reference's synthetic
+        database (client.cpp:16-33)."""
+        d_f, pitch = None, 0
+        if files is not None:
+            f = np.ascontiguousarray(np.asarray(files, np.uint8).reshape(num_files, -1))
+            pitch = f.shape[1]
+            d_f = self.alloc_dev(f.size)
+            self.h2d(d_f, f.reshape(-1))
+        check(self._lib.pir_engine_encode_across_dev(self._h, d_f, pitch, num_files, k),
+              "encode_across")
+
     def shard_row(self, i):
         out = np.empty(self.record_bytes, np.uint8)
         check(self._lib.pir_engine_get_shard_row(self._h, i, out.ctypes.data_as(ctypes.c_void_p)),

@@ -115,21 +115,28 @@ class Client:
         self._lib.encode_across_files_server(ctypes.byref(self.c), ctypes.byref(server.s))
 
     def assembleDPFTreeQueryResponses(self, erasure, responses):
-        """Client decode (client.cpp:211-268): erasure[q-1] = 1 for the servers whose
-        answers are given, responses = [NUM_PARTIES - R][NUM_ROUNDS][ENCODED_FILE_SIZE_BYTES]
-        in increasing server order; returns the FILE_SIZE_BYTES record."""
-        prm = params()
-        nr, nq, efs = prm["NUM_PARTIES"] - prm["R"], prm["NUM_ROUNDS"], prm["ENCODED_FILE_SIZE_BYTES"]
-        resp = np.ascontiguousarray(np.asarray(responses, np.uint8).reshape(nr, nq, efs))
-        er = np.ascontiguousarray(np.asarray(erasure, np.uint8))
-        rows = [(c_u8_p * nq)(*[resp[j, i].ctypes.data_as(c_u8_p) for i in range(nq)]) for j in range(nr)]
-        outer = (ctypes.POINTER(c_u8_p) * nr)(*[ctypes.cast(r, ctypes.POINTER(c_u8_p)) for r in rows])
-        out = np.zeros(_lib.global_int("FILE_SIZE_BYTES"), np.uint8)
-        self._lib.assembleDPFTreeQueryResponses(ctypes.byref(self.c),
-                                                er.ctypes.data_as(ctypes.c_void_p), outer,
-                                                out.ctypes.data_as(ctypes.c_void_p))
-        return out
+        """Client decode (client.cpp:211-268); see the module function of the same name."""
+        return assembleDPFTreeQueryResponses(erasure, responses, self.c)
 
     def free_client(self):
         if self.c.unencoded_files:
             self._lib.free_client(ctypes.byref(self.c))
+
+
+def assembleDPFTreeQueryResponses(erasure, responses, c=None):
+    """Client erasure decode of one tree-mode query (client.cpp:211-268) under the current
+    setSystemParams: erasure[q-1] = 1 for the servers whose answers are given, responses =
+    [NUM_PARTIES - R][NUM_ROUNDS][ENCODED_FILE_SIZE_BYTES] in increasing server order.  Returns
+    the FILE_SIZE_BYTES record.  The decode reads no client state, so `c` may be omitted."""
+    lib = _lib.load()
+    prm = params()
+    nr, nq, efs = prm["NUM_PARTIES"] - prm["R"], prm["NUM_ROUNDS"], prm["ENCODED_FILE_SIZE_BYTES"]
+    resp = np.ascontiguousarray(np.asarray(responses, np.uint8).reshape(nr, nq, efs))
+    er = np.ascontiguousarray(np.asarray(erasure, np.uint8))
+    rows = [(c_u8_p * nq)(*[resp[j, i].ctypes.data_as(c_u8_p) for i in range(nq)]) for j in range(nr)]
+    outer = (ctypes.POINTER(c_u8_p) * nr)(*[ctypes.cast(r, ctypes.POINTER(c_u8_p)) for r in rows])
+    out = np.zeros(_lib.global_int("FILE_SIZE_BYTES"), np.uint8)
+    cl = c if c is not None else CClient()
+    lib.assembleDPFTreeQueryResponses(ctypes.byref(cl), er.ctypes.data_as(ctypes.c_void_p), outer,
+                                      out.ctypes.data_as(ctypes.c_void_p))
+    return out

@@ -68,6 +68,13 @@ int pir_engine_set_shard_rows(pir_engine_t *e, const uint8_t *const *rows, uint6
 /* synthetic shard generated on the device (bench): byte b of GLOBAL row i is a function of
  * (seed, i, b), so every partition of a logical shard agrees with the whole */
 int pir_engine_fill_shard_random(pir_engine_t *e, uint64_t seed);
+/* the server's erasure-coded shard, computed on the GPU (client.cpp:70-97, the server setup of
+ * src/server/server.go:299-331): global row r = XOR_{j<k, src = encdb*j + r < num_files}
+ * gf_pow(party_index, j) * file[src], encdb = ceil(num_files / k), for this engine's rows.
+ * d_files: num_files device rows file_pitch bytes apart (record_bytes used), or NULL for the
+ * reference's synthetic database (client.cpp:16-33). */
+int pir_engine_encode_across_dev(pir_engine_t *e, const uint8_t *d_files, uint64_t file_pitch,
+                                 uint64_t num_files, int k);
 int pir_engine_get_shard_row(pir_engine_t *e, uint64_t row, uint8_t *out);
 /* rows [row0, row0+nrows) back to the host, record_bytes per row, packed */
 int pir_engine_get_shard(pir_engine_t *e, uint64_t row0, uint64_t nrows, uint8_t *out);
