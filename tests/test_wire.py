@@ -1,0 +1,120 @@
+"""The wire boundary: `pir_serve` (C++, TLS + msgpack framing of src/server/server.go:53-125)
+and the Python client of erasurecodedpir_amd/wire.py (src/client/tree.go).  On the CPU: the
+TLS handshake, the request framing and the TEST echo, and that a setup without a GPU fails
+loudly.  On the GPU: the configs[0] loopback (2 servers, 2^16 x 256 B, one query) and an
+erasure-coded setup with a server down, decoded from the remaining answers."""
+import os
+import socket
+import subprocess
+import time
+
+import numpy as np
+import pytest
+
+from erasurecodedpir_amd import wire
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SERVE = os.path.join(ROOT, "erasurecodedpir_amd", "pir_serve")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class Servers:
+    def __init__(self, p, byzantine=()):
+        self.procs, self.addrs = [], []
+        for party in range(1, p + 1):
+            port = _free_port()
+            args = [SERVE, "--port", str(port), "--party", str(party)]
+            if party in byzantine:
+                args += ["--byzantine", "1"]
+            self.procs.append(subprocess.Popen(args, stderr=subprocess.PIPE))
+            self.addrs.append(("127.0.0.1", port))
+        for addr in self.addrs:  # wait until listening
+            for _ in range(200):
+                try:
+                    socket.create_connection(addr, timeout=1).close()
+                    break
+                except OSError:
+                    time.sleep(0.05)
+
+    def stop(self, i):
+        self.procs[i].terminate()
+        self.procs[i].wait(timeout=30)
+
+    def close(self):
+        for pr in self.procs:
+            if pr.poll() is None:
+                pr.terminate()
+                try:
+                    pr.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    pr.kill()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+@pytest.fixture(scope="module")
+def serve_bin():
+    if not os.path.exists(SERVE):
+        pytest.fail("pir_serve not built (make -C erasurecodedpir_amd/csrc)")
+    return SERVE
+
+
+def test_tls_framing_and_echo(serve_bin):
+    with Servers(1) as sv:
+        with wire.Conn(*sv.addrs[0]) as c:
+            for msg in ("", "hello", "x" * 5000):
+                assert c.call(wire.TEST_REQUEST, {"Msg": msg}) == {"Msg": msg}
+
+
+def test_setup_without_gpu_fails_loudly(serve_bin):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with Servers(1) as sv:
+        with pytest.raises(wire.WireError):
+            wire.setup(sv.addrs[0], 10, 16, 1, 0)
+        with pytest.raises(wire.WireError):  # no engine: a query is refused, not answered
+            wire.tree_search(sv.addrs[0], b"\0" * 100)
+
+
+def _synthetic(v, f):  # client.cpp:16-33
+    return np.arange(f, dtype=np.uint8) if v == 1 else np.full(f, v & 0xFF, np.uint8)
+
+
+@pytest.mark.gpu
+def test_loopback_configs0(serve_bin):
+    """BASELINE configs[0]: 2-server loopback, 2^16 x 256 B database, queries decoded."""
+    L, f, k, r = 16, 256, 1, 0
+    with Servers(2) as sv:
+        for addr in sv.addrs:
+            resp = wire.setup(addr, L, f, k, r)
+            assert resp["ServerLatency"] >= 0
+        for idx in (1, 5, 40000, (1 << L) - 1):
+            rec, resps, er = wire.tree_query(sv.addrs, idx, L, f, k, r)
+            assert er == [1, 1]
+            assert np.array_equal(rec, _synthetic(idx, f)), idx
+            assert {r_["PartyIndex"] for r_ in resps} == {1, 2}
+
+
+@pytest.mark.gpu
+def test_erasure_coded_servers_with_one_down(serve_bin):
+    """k=3, r=1 -> p=5 servers, NUM_ROUNDS=3; one server killed before the query."""
+    L, f, k, r = 14, 128, 3, 1
+    with Servers(5) as sv:
+        for addr in sv.addrs:
+            wire.setup(addr, L, f, k, r)
+        sv.stop(2)
+        encdb = -(-(1 << L) // k)
+        for row in (1, 7, encdb - 1):
+            rec, _, er = wire.tree_query(sv.addrs, row, L, f, k, r)
+            assert er[2] == 0 and sum(er) == 4
+            assert np.array_equal(rec, _synthetic(row, f)), row
