@@ -114,6 +114,8 @@ struct pir_engine {
   int last_batch_group = 0;
   int batch_scan_bpc = 2;       // scan workgroups per CU in batched answers ($PIR_BATCH_SCAN_BPC)
   uint8_t* d_result = nullptr;  // nq*efs (host-API staging)
+  uint8_t* d_qscratch = nullptr;  // k_query super-tile tile inputs
+  size_t qscratch_cap = 0;
   uint8_t* h_key = nullptr;     // pinned
   uint8_t* h_res = nullptr;     // pinned
   std::vector<DevBuf> user;     // pir_engine_alloc_dev
@@ -241,6 +243,7 @@ int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, 
   const auto& c = e->cfg;
   const pir::ScanShape& sh = qp.shape;
   int rc = ensure_slabs(e, (size_t)nk * pir::query_slab_bytes(qp));
+  if (!rc) rc = ensure_buf(&e->d_qscratch, &e->qscratch_cap, pir::query_scratch_bytes(qp));
   if (rc) return rc;
   e->last_chunks = 1;
   e->last_fused = 2;
@@ -254,7 +257,7 @@ int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, 
   }
   HIP_TRY(pir::launch_query(qp, d_raw, (uint32_t)e->key_len, nk, c.num_parties,
                             c.log_num_records, c.party_index - 1, log_parts_total, prefix,
-                            e->d_shard + row0 * e->pitch, e->d_slabs, s));
+                            e->d_shard + row0 * e->pitch, e->d_slabs, e->d_qscratch, s));
   if (ev) {
     HIP_TRY(hipEventRecord(ev[EV_SCAN_E], s));
     HIP_TRY(hipEventRecord(ev[EV_PRERED], s));
@@ -654,7 +657,7 @@ void pir_engine_destroy(pir_engine_t* e) {
                   (void*)e->nodes.s[0], (void*)e->nodes.s[1], (void*)e->nodes.t[0],
                   (void*)e->nodes.t[1], (void*)e->d_c, (void*)e->d_slabs, (void*)e->d_part,
                   (void*)e->d_gather, (void*)e->d_result, (void*)e->d_cb, (void*)e->d_gtmp,
-                  (void*)e->d_bpart, (void*)e->d_bgather, (void*)e->bnodes.s[0],
+                  (void*)e->d_bpart, (void*)e->d_bgather, (void*)e->d_qscratch, (void*)e->bnodes.s[0],
                   (void*)e->bnodes.s[1], (void*)e->bnodes.t[0], (void*)e->bnodes.t[1]})
     if (p) (void)hipFree(p);
   for (auto& b : e->user) (void)hipFree(b.p);
@@ -990,17 +993,23 @@ int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, int num_keys, 
   if (!qp.tile) return fail(PIR_EINVAL, "shape does not use the single-launch query kernel");
   const pir::ScanShape& sh = qp.shape;
   int rc = ensure_slabs(e, (size_t)num_keys * pir::query_slab_bytes(qp));
+  if (!rc) rc = ensure_buf(&e->d_qscratch, &e->qscratch_cap, pir::query_scratch_bytes(qp));
   if (rc) return rc;
   const int nwg = (int)sh.grid.x;
   const size_t bytes = (size_t)nwg * pir::kQueryTraceSlots * sizeof(uint64_t);
   uint64_t* d_tr = nullptr;
-  HIP_TRY(hipMalloc(&d_tr, bytes));
+  HIP_TRY(hipMalloc(&d_tr, bytes + sizeof(uint64_t)));
   std::vector<uint64_t> h((size_t)nwg * pir::kQueryTraceSlots);
   hipError_t err = hipMemsetAsync(d_tr, 0, bytes, e->stream);
+  const char* dbg = getenv("PIR_TRACE_NOSCAN");  // diagnostics: scan waves skip their rows
+  const uint64_t flags = (dbg && dbg[0] == '1') ? 1u : 0u;
+  if (err == hipSuccess)
+    err = hipMemcpyAsync(d_tr + (size_t)nwg * pir::kQueryTraceSlots, &flags, sizeof flags,
+                         hipMemcpyHostToDevice, e->stream);
   if (err == hipSuccess)
     err = pir::launch_query(qp, d_key, (uint32_t)e->key_len, num_keys, c.num_parties, c.log_num_records,
                             c.party_index - 1, c.log_num_partitions, (uint64_t)c.partition_index,
-                            e->d_shard, e->d_slabs, e->stream, d_tr);
+                            e->d_shard, e->d_slabs, e->d_qscratch, e->stream, d_tr);
   if (err == hipSuccess) err = hipMemcpyAsync(h.data(), d_tr, bytes, hipMemcpyDeviceToHost, e->stream);
   if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
   (void)hipFree(d_tr);

@@ -111,6 +111,7 @@ hipError_t launch_fused(const TreePlan& pl, const DevKey* d_key, const NodeBufs&
 // tile == 0: shape not supported.
 struct QueryPlan {
   int tile, lr, lt;
+  int ls;           // 2^ls tiles per super-tile (their narrow top levels expanded once)
   int tw;           // tree waves per workgroup (the rest scan)
   ScanShape shape;  // grid.x = 2^lr workgroups (slabs), grid.y = column groups
 };
@@ -120,9 +121,11 @@ inline size_t query_slab_bytes(const QueryPlan& qp) {
   return (size_t)qp.shape.grid.x * qp.shape.grid.y * qp.shape.slab_bytes;
 }
 constexpr int kQueryTraceSlots = 192;  // trace: per-workgroup phase stamps (wall clock, 100 MHz)
+// device scratch for the super-tile tile inputs (0 when ls == 0)
+size_t query_scratch_bytes(const QueryPlan& qp);
 hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
                         int p, int n, int party0, int log_parts, uint64_t prefix,
-                        const uint8_t* shard, uint8_t* slabs, hipStream_t s,
+                        const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
                         uint64_t* trace = nullptr);
 // XOR the slabs, compact pitch -> record_bytes: d_out[a*efs + b]; nk queries (slabs of query k
 // grid.x*grid.y*slab_bytes apart, answers nq*efs bytes apart)

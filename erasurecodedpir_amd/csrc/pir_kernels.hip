@@ -842,6 +842,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
 // write the workgroup's partial answer (slab) of that query.
 // ------------------------------------------------------------------------------------------
 constexpr int kQueryCwCap = 256;  // (levels x (p-1)) correction words staged in LDS
+constexpr int kQueryKin = 6;      // a tile's input nodes sit 6 levels below its root (64 of them)
 
 template <int TILE, int NRP, int NQ, int VEC, int GYMAX, int RING>
 struct QuerySmem {
@@ -894,11 +895,15 @@ __device__ __forceinline__ void stage_key(const uint8_t* __restrict__ raw, int p
 template <int NQ, int NRP, int VEC, bool UNI, int TW, int TILE, int GYMAX, int RING>
 __global__ __launch_bounds__(kFusedThreads) void k_query(
     const uint8_t* __restrict__ raw0, uint32_t key_stride, int nk, int p, int n, int nq,
-    int party0, int log_parts, uint64_t prefix, int lr, int lt, const uint8_t* __restrict__ shard,
+    int party0, int log_parts, uint64_t prefix, int lr, int lt, int ls,
+    uint4* __restrict__ fr_s, uint32_t* __restrict__ fr_t, const uint8_t* __restrict__ shard,
     uint32_t pitch, uint32_t cpr, uint32_t gy, uint8_t* __restrict__ slabs,
     uint64_t* __restrict__ trace) {
   // trace != nullptr: per-workgroup wall-clock stamps (100 MHz) of query 0's phases,
   // kQueryTraceSlots apart (layout: pir_engine_trace_query, include/pir_engine.h)
+  // diagnostics only: trace[kQueryTraceSlots * gridDim.x] bit 0 = scan waves skip their rows
+  // (wrong answers; isolates the tree's rate beside the scan)
+  const bool trace_flags_noscan = trace && (trace[(uint64_t)kQueryTraceSlots * gridDim.x] & 1u);
   if (trace) trace += (uint64_t)blockIdx.x * kQueryTraceSlots;
   if (trace && threadIdx.x == 0) { trace[0] = wall_clock64(); trace[56] = clock64(); }
   constexpr int SW = kFusedWaves - TW;
@@ -924,6 +929,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
   const uint64_t b = blockIdx.x;
   const uint32_t ntiles = 1u << lt;
   const uint32_t total = ntiles * (uint32_t)nk;  // tiles of the whole queue
+  if (ls) {  // this workgroup's super-tile scratch (64 << ls nodes)
+    fr_s += (size_t)b << (kQueryKin + ls);
+    fr_t += (size_t)b << (kQueryKin + ls);
+  }
   const uint64_t region_rows = (uint64_t)TILE << lt;
   const size_t slab_words = (size_t)NQ * GW;
   const size_t slab_q_words = (size_t)gy * gridDim.x * slab_words;  // one query's slabs
@@ -953,13 +962,13 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
   auto cw = [&](int L, uint32_t tv, uint4& cs, uint32_t& ct) {
     cw_lds(sm.scw, sm.tcw, L, tv, pm1, cs, ct);
   };
-  auto tree_tile = [&](uint32_t g, int nt, uint32_t team) {
+  auto tree_tile = [&](uint32_t g, int nt, uint32_t team) __attribute__((always_inline)) {
     const uint32_t i = g % ntiles;
     const uint8_t* raw = raw0 + (size_t)(g / ntiles) * key_stride;
     uint8_t* ring = sm.ring[g % RING];
     // the whole workgroup: hardware barrier (waiting waves sleep); the tree waves alone: LDS
     // counter barrier (the scan waves keep streaming)
-    auto sync = [&]() {
+    auto sync = [&]() __attribute__((always_inline)) {
       if (team == (uint32_t)kFusedWaves) __syncthreads();
       else group_barrier(&sm.bar, gen, team);
     };
@@ -967,127 +976,164 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
       stage_key(raw, p, n, nq, tt, nt, sm.scw, sm.tcw, sm.lastcw);  // are past its last use)
       sync();
     }
-    // ---- tile root (wave 0, column shape, depth-first) ------------------------------------
-    if (wave == 0) {
-      int L0, depth;
-      uint32_t sq, t;
-      uint64_t path;  // bits of the levels still to descend (MSB first)
-      if (i == 0) {
-        L0 = 0;
-        depth = Lt;
-        sq = load_le32(raw + 4 * q);
-        t = party0 >= 1 ? (1u << (party0 - 1)) : 0u;  // dpf_tree.cpp:496-502
-        path = (((prefix << lr) | b) << lt);
-      } else {
-        const int j = __builtin_ctz(i);
-        L0 = Lt - j;  // the right sibling popped at level L0, then j left turns
-        depth = j;
-        sq = reinterpret_cast<const uint32_t*>(&sm.stk_s[L0])[q];
-        t = sm.stk_t[L0];
-        path = 0;
-      }
-      // the 4 groups of 16 lanes compute the same node; the path bit is wave-uniform, so the
-      // chosen child moves to every lane through SGPRs (v_readlane), not through the LDS
-      const uint32_t m0 = q == 0 ? ~0u : 0u, m1 = q == 1 ? ~0u : 0u;
-      const uint32_t m2 = q == 2 ? ~0u : 0u, m3 = q == 3 ? ~0u : 0u;
-      for (int d = 0; d < depth; ++d) {
-        const int L = L0 + d;
-        // word q of the correction word (t is wave-uniform here); issued before the rounds
-        uint32_t csq = 0, ct = 0;
-        for (uint32_t j = 0; j < pm1; ++j) {
-          const uint32_t m = 0u - ((t >> j) & 1u);
-          csq ^= reinterpret_cast<const uint32_t*>(&sm.scw[L * (int)pm1 + (int)j])[q] & m;
-          ct ^= sm.tcw[L * (int)pm1 + (int)j] & m;
-        }
-        const uint32_t o = aes_col(T, sq, ptq, mq1, mq2);
-        const uint32_t bit = (uint32_t)((path >> (depth - 1 - d)) & 1u);
-        const uint32_t oc = o ^ csq;
-        const uint32_t tbits = (__builtin_amdgcn_readlane(o, 8) & B.tb_mask) ^
-                               __builtin_amdgcn_readfirstlane(ct);
-        if (L >= Lr && bit == 0) {  // inside the region: keep the right child for later tiles
-          if (lane >= 4 && lane < 8) reinterpret_cast<uint32_t*>(&sm.stk_s[L + 1])[lane - 4] = oc;
-          if (lane == 0) sm.stk_t[L + 1] = (tbits >> pm1) & B.tmask;
-        }
-        const uint32_t c0 = __builtin_amdgcn_readlane(oc, (int)(4 * bit + 0));
-        const uint32_t c1 = __builtin_amdgcn_readlane(oc, (int)(4 * bit + 1));
-        const uint32_t c2 = __builtin_amdgcn_readlane(oc, (int)(4 * bit + 2));
-        const uint32_t c3 = __builtin_amdgcn_readlane(oc, (int)(4 * bit + 3));
-        sq = (c0 & m0) | (c1 & m1) | (c2 & m2) | (c3 & m3);
-        t = (tbits >> (bit * pm1)) & B.tmask;
-        if (trace && g == 0 && lane == 0 && d < 32) trace[8 + d] = wall_clock64();
-      }
-      uint4* s0 = ((KT - 1) & 1) ? sm.sb : sm.sa;
-      uint32_t* t0 = ((KT - 1) & 1) ? sm.tb : sm.ta;
-      if (lane < 4) reinterpret_cast<uint32_t*>(&s0[0])[lane] = sq;
-      if (lane == 0) t0[0] = t;
-      if (trace && g == 0 && lane == 0) { trace[2] = wall_clock64(); trace[57] = clock64(); }
-    }
-    sync();
-    if (trace && g == 1 && tt == 0) trace[176] = wall_clock64();
-    // ---- breadth-first expansion of the tile root ------------------------------------------
-    // level i of a tile (width 2^i) lives in buffer a when (KT-1-i) is even, else b
-    int buf = (KT - 1) & 1;
-    int W = 1;
-    for (int lv = 0; lv < KT - 1; ++lv) {
-      const int L = Lt + lv;
-      const uint4* is = buf ? sm.sb : sm.sa;
-      const uint32_t* it = buf ? sm.tb : sm.ta;
-      uint4* os = buf ? sm.sa : sm.sb;
-      uint32_t* ot = buf ? sm.ta : sm.tb;
-      if (W * 16 <= nt) {  // column shape: 16 lanes per node
-        const int u = tt >> 4;
-        if (u < W) {  // uniform per 16-lane group
-          const uint32_t s_in = reinterpret_cast<const uint32_t*>(&is[u])[q], t_in = it[u];
-          uint4 cs;
-          uint32_t ct;
-          cw(L, t_in, cs, ct);
-          const uint32_t o = aes_col(T, s_in, ptq, mq1, mq2);
-          if (role < 2) {
-            reinterpret_cast<uint32_t*>(&os[2 * u + role])[q] = o ^ word_of(cs, q);
-          } else if (role == 2 && q == 0) {
-            const uint32_t tb = (o & B.tb_mask) ^ ct;
+    // ---- breadth-first expansion of a subtree, relative levels m0 -> mlast ----------------
+    // (level m of the span, width 2^m, lives in buffer a when (mlast - m) is even, else b, so
+    // the span's last level ends in a; absolute level = Lspan + m)
+    int tl = 0;  // levels expanded so far in this tile (trace)
+    auto expand_span = [&](int Lspan, int m0, int mlast) __attribute__((always_inline)) {
+      for (int m = m0; m < mlast; ++m) {
+        const int W = 1 << m, L = Lspan + m;
+        const bool inb = (mlast - m) & 1;
+        const uint4* is = inb ? sm.sb : sm.sa;
+        const uint32_t* it = inb ? sm.tb : sm.ta;
+        uint4* os = inb ? sm.sa : sm.sb;
+        uint32_t* ot = inb ? sm.ta : sm.tb;
+        if (W * 16 <= nt) {  // column shape: 16 lanes per node
+          const int u = tt >> 4;
+          if (u < W) {  // uniform per 16-lane group
+            const uint32_t s_in = reinterpret_cast<const uint32_t*>(&is[u])[q], t_in = it[u];
+            uint4 cs;
+            uint32_t ct;
+            cw(L, t_in, cs, ct);
+            const uint32_t o = aes_col(T, s_in, ptq, mq1, mq2);
+            if (role < 2) {
+              reinterpret_cast<uint32_t*>(&os[2 * u + role])[q] = o ^ word_of(cs, q);
+            } else if (role == 2 && q == 0) {
+              const uint32_t tb = (o & B.tb_mask) ^ ct;
+              ot[2 * u] = tb & B.tmask;
+              ot[2 * u + 1] = (tb >> B.pm1) & B.tmask;
+            }
+          }
+        } else if (W <= (nt >> 6) * 21) {
+          // 3 lanes per node, lane r runs CTR block r with its own key schedule: two thirds of
+          // the row-shape latency for a level that fits the team in one pass
+          const int l = tt & 63, ul = l / 3, r = l - 3 * ul;
+          const int npp = (nt >> 6) * 21;
+          for (int u = (tt >> 6) * 21 + ul; l < 63 && u < W; u += npp) {
+            uint4 cs;
+            uint32_t ct;
+            cw(L, it[u], cs, ct);
+            const uint4 o = aes_ctr_block(T, is[u], (uint32_t)r);
+            if (r < 2) {
+              os[2 * u + r] = xor4(o, cs);
+            } else {
+              const uint32_t tb = (o.x & B.tb_mask) ^ ct;
+              ot[2 * u] = tb & B.tmask;
+              ot[2 * u + 1] = (tb >> B.pm1) & B.tmask;
+            }
+          }
+        } else {  // row shape: one lane per node, 3 CTR blocks on one key schedule
+          for (int u = tt; u < W; u += nt) {
+            uint4 cs;
+            uint32_t ct;
+            cw(L, it[u], cs, ct);
+            uint4 o[3];
+            aes_ctr_row<3, 1>(T, is[u], o);
+            const uint32_t tb = (o[2].x & B.tb_mask) ^ ct;
+            os[2 * u] = xor4(o[0], cs);
+            os[2 * u + 1] = xor4(o[1], cs);
             ot[2 * u] = tb & B.tmask;
             ot[2 * u + 1] = (tb >> B.pm1) & B.tmask;
           }
         }
-      } else if (W <= (nt >> 6) * 21) {
-        // 3 lanes per node, lane r runs CTR block r with its own key schedule: two thirds of
-        // the row-shape latency for a level that fits the team in one pass
-        const int l = tt & 63, ul = l / 3, r = l - 3 * ul;
-        const int npp = (nt >> 6) * 21;
-        for (int u = (tt >> 6) * 21 + ul; l < 63 && u < W; u += npp) {
-          uint4 cs;
-          uint32_t ct;
-          cw(L, it[u], cs, ct);
-          const uint4 o = aes_ctr_block(T, is[u], (uint32_t)r);
-          if (r < 2) {
-            os[2 * u + r] = xor4(o, cs);
-          } else {
-            const uint32_t tb = (o.x & B.tb_mask) ^ ct;
-            ot[2 * u] = tb & B.tmask;
-            ot[2 * u + 1] = (tb >> B.pm1) & B.tmask;
+        sync();
+        if (trace && g == 0 && tt == 0 && tl < 16) trace[40 + tl] = wall_clock64();
+        if (trace && g == 1 && tt == 0 && tl < 16) trace[160 + tl] = wall_clock64();
+        ++tl;
+      }
+    };
+    // ---- super-tile root (wave 0, column shape, depth-first) ------------------------------
+    // Super-tile j = i >> ls (2^ls tiles, root at level Ls) is expanded once down to the 64
+    // input nodes of each of its tiles; j == 0 descends all Ls levels from the root along
+    // (prefix, b, 0); j > 0 pops the right sibling stored when its ancestor was expanded and
+    // descends ctz(j) levels, so the super-tile roots cost (#super-tiles - 1) expansions.
+    const uint32_t smask = (1u << ls) - 1u;
+    const int Ls = Lt - ls;
+    const int span_last = ls ? ls + kQueryKin : KT - 1;  // relative last level of the root span
+    if ((i & smask) == 0) {
+      const uint32_t j = i >> ls;
+      if (wave == 0) {
+        int L0, depth;
+        uint32_t sq, t;
+        uint64_t path;  // bits of the levels still to descend (MSB first)
+        if (j == 0) {
+          L0 = 0;
+          depth = Ls;
+          sq = load_le32(raw + 4 * q);
+          t = party0 >= 1 ? (1u << (party0 - 1)) : 0u;  // dpf_tree.cpp:496-502
+          path = (((prefix << lr) | b) << (lt - ls));
+        } else {
+          const int c = __builtin_ctz(j);
+          L0 = Ls - c;  // the right sibling popped at level L0, then c left turns
+          depth = c;
+          sq = reinterpret_cast<const uint32_t*>(&sm.stk_s[L0])[q];
+          t = sm.stk_t[L0];
+          path = 0;
+        }
+        // the 4 groups of 16 lanes compute the same node; the path bit is wave-uniform, so the
+        // chosen child moves to every lane through SGPRs (v_readlane), not through the LDS
+        const uint32_t m0 = q == 0 ? ~0u : 0u, m1 = q == 1 ? ~0u : 0u;
+        const uint32_t m2 = q == 2 ? ~0u : 0u, m3 = q == 3 ? ~0u : 0u;
+        for (int d = 0; d < depth; ++d) {
+          const int L = L0 + d;
+          // word q of the correction word (t is wave-uniform here); issued before the rounds
+          uint32_t csq = 0, ct = 0;
+          for (uint32_t jj = 0; jj < pm1; ++jj) {
+            const uint32_t m = 0u - ((t >> jj) & 1u);
+            csq ^= reinterpret_cast<const uint32_t*>(&sm.scw[L * (int)pm1 + (int)jj])[q] & m;
+            ct ^= sm.tcw[L * (int)pm1 + (int)jj] & m;
           }
+          const uint32_t o = aes_col(T, sq, ptq, mq1, mq2);
+          const uint32_t bit = (uint32_t)((path >> (depth - 1 - d)) & 1u);
+          const uint32_t oc = o ^ csq;
+          const uint32_t tbits = (__builtin_amdgcn_readlane(o, 8) & B.tb_mask) ^
+                                 __builtin_amdgcn_readfirstlane(ct);
+          if (L >= Lr && bit == 0) {  // inside the region: keep the right child for later
+            if (lane >= 4 && lane < 8) reinterpret_cast<uint32_t*>(&sm.stk_s[L + 1])[lane - 4] = oc;
+            if (lane == 0) sm.stk_t[L + 1] = (tbits >> pm1) & B.tmask;
+          }
+          const uint32_t c0 = __builtin_amdgcn_readlane(oc, (int)(4 * bit + 0));
+          const uint32_t c1 = __builtin_amdgcn_readlane(oc, (int)(4 * bit + 1));
+          const uint32_t c2 = __builtin_amdgcn_readlane(oc, (int)(4 * bit + 2));
+          const uint32_t c3 = __builtin_amdgcn_readlane(oc, (int)(4 * bit + 3));
+          sq = (c0 & m0) | (c1 & m1) | (c2 & m2) | (c3 & m3);
+          t = (tbits >> (bit * pm1)) & B.tmask;
+          if (trace && g == 0 && lane == 0 && d < 32) trace[8 + d] = wall_clock64();
         }
-      } else {  // row shape: one lane per node, 3 CTR blocks on one key schedule
-        for (int u = tt; u < W; u += nt) {
-          uint4 cs;
-          uint32_t ct;
-          cw(L, it[u], cs, ct);
-          uint4 o[3];
-          aes_ctr_row<3, 1>(T, is[u], o);
-          const uint32_t tb = (o[2].x & B.tb_mask) ^ ct;
-          os[2 * u] = xor4(o[0], cs);
-          os[2 * u + 1] = xor4(o[1], cs);
-          ot[2 * u] = tb & B.tmask;
-          ot[2 * u + 1] = (tb >> B.pm1) & B.tmask;
-        }
+        uint4* s0 = (span_last & 1) ? sm.sb : sm.sa;
+        uint32_t* t0 = (span_last & 1) ? sm.tb : sm.ta;
+        if (lane < 4) reinterpret_cast<uint32_t*>(&s0[0])[lane] = sq;
+        if (lane == 0) t0[0] = t;
+        if (trace && g == 0 && lane == 0) { trace[2] = wall_clock64(); trace[57] = clock64(); }
       }
       sync();
-      if (trace && g == 0 && tt == 0 && lv < 16) trace[40 + lv] = wall_clock64();
-      if (trace && g == 1 && tt == 0 && lv < 16) trace[160 + lv] = wall_clock64();
-      buf ^= 1;
-      W *= 2;
+      if (trace && g == 1 && tt == 0) trace[176] = wall_clock64();
+      if (ls) {  // the super-tile's top: 2^ls x 64 tile inputs, once, to the scratch
+        expand_span(Ls, 0, span_last);
+        const int nf = 64 << ls;
+        for (int u = tt; u < nf; u += nt) {
+          fr_s[u] = sm.sa[u];
+          fr_t[u] = sm.ta[u];
+        }
+        sync();
+      }
     }
+    if (ls) {  // this tile's 64 input nodes (relative level kQueryKin) from the scratch
+      const bool inb = (KT - 1 - kQueryKin) & 1;
+      uint4* s0 = inb ? sm.sb : sm.sa;
+      uint32_t* t0 = inb ? sm.tb : sm.ta;
+      const int base = (int)(i & smask) * 64;
+      for (int u = tt; u < 64; u += nt) {
+        s0[u] = fr_s[base + u];
+        t0[u] = fr_t[base + u];
+      }
+      sync();
+      expand_span(Lt, kQueryKin, KT - 1);
+    } else {
+      expand_span(Lt, 0, KT - 1);
+    }
+    const int buf = 0;            // the leaf parents (relative level KT - 1) are in buffer a
+    const int W = 1 << (KT - 1);  // ... TILE / 2 of them
     // ---- last level + leaf conversion (dpf_tree.cpp:567-580) into the ring -----------------
     // c[leaf][a] = AES_{s_leaf}(0)[a] ^ XOR_{k: t_leaf bit k} lastCW[k][a]   (a < nq)
     {
@@ -1193,7 +1239,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
       const uint32_t i = g % ntiles;
       const uint8_t* ring = sm.ring[g % RING];
       lds_wait_geq(&sm.ready, g + 1);
-      if (wi < nwg) {
+      if (wi < nwg && !(trace && trace_flags_noscan)) {
         const uint8_t* base = rbase + ((uint64_t)i * TILE) * pitch;
         for (uint32_t g0 = wi; g0 < ngroups; g0 += U * nwg) {
           Chunk<VEC> x[U];
@@ -1601,6 +1647,15 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
   qp.tile = tile;
   qp.lr = lr;
   qp.lt = nr - kt - lr;
+  // super-tiles of 2^ls tiles share their narrow top levels (expanded once, to 64 input nodes
+  // per tile); 64 << ls nodes must fit the LDS level buffer of TILE / 2 ($PIR_QUERY_SUPER=0: off)
+  // Only where the tree, not the scan, paces the launch (small records, or a queue): a lone
+  // query of large records waits for its first tile, and a super-tile's top is wider than one
+  // tile's.
+  qp.ls = std::min(qp.lt, kt - 1 - kQueryKin);
+  if (nk == 1 && !(nq <= 2 && pitch <= 256)) qp.ls = 0;
+  if (const char* sv = getenv("PIR_QUERY_SUPER"))
+    if (sv[0] == '0') qp.ls = 0;
   qp.shape = make_fused_shape(nleaves, pitch, nq, num_cus, tile);
   qp.shape.grid.x = 1u << lr;
   return qp;
@@ -1609,7 +1664,10 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
 template <int NQ, int TILE>
 static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
                            int p, int n, int party0, int log_parts, uint64_t prefix,
-                           const uint8_t* shard, uint8_t* slabs, hipStream_t s, uint64_t* trace) {
+                           const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
+                           uint64_t* trace) {
+  uint4* fr_s = reinterpret_cast<uint4*>(scratch);
+  uint32_t* fr_t = reinterpret_cast<uint32_t*>(scratch + ((size_t)qp.shape.grid.x << (kQueryKin + qp.ls)) * sizeof(uint4));
   constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : 8));
   constexpr int VEC = NQ <= 2 ? 4 : 2;
   constexpr int RING = TILE == 4096 ? 2 : 4;  // share slots: the tree runs RING-1 tiles ahead
@@ -1617,7 +1675,8 @@ static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t k
 #define PIR_QL(UNI, TW, GY, gy)                                                                  \
   hipLaunchKernelGGL((k_query<NQ, NRP, VEC, UNI, TW, TILE, GY, RING>), dim3(sh.grid.x),          \
                      dim3(kFusedThreads), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,          \
-                     log_parts, prefix, qp.lr, qp.lt, shard, sh.pitch, sh.cpr, gy, slabs, trace)
+                     log_parts, prefix, qp.lr, qp.lt, qp.ls, fr_s, fr_t, shard, sh.pitch, sh.cpr,  \
+                     gy, slabs, trace)
   if constexpr (NQ <= 2) {
     if (qp.tw == kQueryTreeHeavyTW) {  // small records: the tree is the bottleneck
       if (sh.uniform) PIR_QL(true, kQueryTreeHeavyTW, 4, sh.grid.y);
@@ -1631,11 +1690,16 @@ static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t k
   return hipGetLastError();
 }
 
+size_t query_scratch_bytes(const QueryPlan& qp) {
+  return qp.ls ? ((size_t)qp.shape.grid.x << (kQueryKin + qp.ls)) * (sizeof(uint4) + sizeof(uint32_t)) : 0;
+}
+
 hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
                         int p, int n, int party0, int log_parts, uint64_t prefix,
-                        const uint8_t* shard, uint8_t* slabs, hipStream_t s, uint64_t* trace) {
-  if (nk < 1) return hipErrorInvalidValue;
-#define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, s, trace)
+                        const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
+                        uint64_t* trace) {
+  if (nk < 1 || (qp.ls && !scratch)) return hipErrorInvalidValue;
+#define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, scratch, s, trace)
   if (qp.tile == 4096) {
     switch (qp.shape.nq) {
       case 1: return PIR_Q(1, 4096);
