@@ -449,6 +449,88 @@ __device__ __forceinline__ uint32_t mxor(uint32_t z, uint32_t x, uint32_t m) {
   return __builtin_amdgcn_bitop3_b32(z, x, m, 0x78);
 }
 
+// The 8 bit-plane masks of every coefficient byte: planes[c][k] = bit k of c ? ~0 : 0.  A
+// wave-uniform coefficient fetches its 8 masks with ONE s_load_dwordx8 instead of 8 s_bfe_i32:
+// the many-round scan issues one SALU op per two v_bitop3 otherwise, and the scalar unit (one
+// per CU) paces it (tools/micro/scan_salu.hip: 1.64 -> 2.87 TB/s at 5 rounds).
+struct PlaneMasks {
+  uint32_t m[256 * 8];
+};
+constexpr PlaneMasks make_plane_masks() {
+  PlaneMasks t{};
+  for (int c = 0; c < 256; ++c)
+    for (int k = 0; k < 8; ++k) t.m[c * 8 + k] = ((c >> k) & 1) ? 0xffffffffu : 0u;
+  return t;
+}
+__constant__ PlaneMasks c_planes = make_plane_masks();
+
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+#ifndef PIR_PLANE_U
+#define PIR_PLANE_U 8
+#endif
+
+// Many-round scan with wave-uniform coefficients: the 8 masks of coefficient byte c come from
+// the table with one s_load_dwordx8, and one asm statement per round folds a row's 2 dwords
+// into that round's 8 planes (16 v_bitop3) while the NEXT round's masks load: the scan waves
+// are latency-bound (2 per SIMD), so a wait per round would stall them.  Left to the compiler,
+// the loads of every round are hoisted ahead and spilled to VGPR lanes (the scan code runs at
+// the SGPR limit).  The asm loads are invisible to the compiler's waitcnt bookkeeping: every
+// statement that reads masks opens with its own s_waitcnt lgkmcnt(0) (which only ever waits
+// longer for the compiler's own LGKM operations), and a loaded tuple is only read by the next
+// statement.
+__device__ __forceinline__ u32x8 plane_masks_issue(uint32_t c) {
+  u32x8 t;
+  asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(t) : "s"(c_planes.m), "s"(c << 5));
+  return t;
+}
+
+#define PIR_FOLD2_BODY                              \
+  "v_bitop3_b32 %0, %0, %17, %19 bitop3:0x78\n\t"   \
+  "v_bitop3_b32 %1, %1, %18, %19 bitop3:0x78\n\t"   \
+  "v_bitop3_b32 %2, %2, %17, %20 bitop3:0x78\n\t"   \
+  "v_bitop3_b32 %3, %3, %18, %20 bitop3:0x78\n\t"   \
+  "v_bitop3_b32 %4, %4, %17, %21 bitop3:0x78\n\t"   \
+  "v_bitop3_b32 %5, %5, %18, %21 bitop3:0x78\n\t"   \
+  "v_bitop3_b32 %6, %6, %17, %22 bitop3:0x78\n\t"   \
+  "v_bitop3_b32 %7, %7, %18, %22 bitop3:0x78\n\t"   \
+  "v_bitop3_b32 %8, %8, %17, %23 bitop3:0x78\n\t"   \
+  "v_bitop3_b32 %9, %9, %18, %23 bitop3:0x78\n\t"   \
+  "v_bitop3_b32 %10, %10, %17, %24 bitop3:0x78\n\t" \
+  "v_bitop3_b32 %11, %11, %18, %24 bitop3:0x78\n\t" \
+  "v_bitop3_b32 %12, %12, %17, %25 bitop3:0x78\n\t" \
+  "v_bitop3_b32 %13, %13, %18, %25 bitop3:0x78\n\t" \
+  "v_bitop3_b32 %14, %14, %17, %26 bitop3:0x78\n\t" \
+  "v_bitop3_b32 %15, %15, %18, %26 bitop3:0x78"
+#define PIR_FOLD2_Z                                                                          \
+  "+v"(Z[0][0]), "+v"(Z[0][1]), "+v"(Z[1][0]), "+v"(Z[1][1]), "+v"(Z[2][0]), "+v"(Z[2][1]),   \
+      "+v"(Z[3][0]), "+v"(Z[3][1]), "+v"(Z[4][0]), "+v"(Z[4][1]), "+v"(Z[5][0]), "+v"(Z[5][1]), \
+      "+v"(Z[6][0]), "+v"(Z[6][1]), "+v"(Z[7][0]), "+v"(Z[7][1])
+#define PIR_FOLD2_IN                                                                         \
+  "v"(x0), "v"(x1), "s"(m[0]), "s"(m[1]), "s"(m[2]), "s"(m[3]), "s"(m[4]), "s"(m[5]), "s"(m[6]), \
+      "s"(m[7])
+
+// wait for m, start loading the masks of coefficient byte cn, fold one round (operand 16 is the
+// next tuple, so the body's operand numbers match planes_fold2's)
+__device__ __forceinline__ u32x8 planes_fold2_next(uint32_t (&Z)[8][2], uint32_t x0, uint32_t x1,
+                                                   const u32x8& m, uint32_t cn) {
+  u32x8 nx;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\t"
+               "s_load_dwordx8 %16, %27, %28\n\t" PIR_FOLD2_BODY
+               : PIR_FOLD2_Z, "=&s"(nx)
+               : PIR_FOLD2_IN, "s"(c_planes.m), "s"(cn << 5));
+  return nx;
+}
+// wait for m and fold one round (no next load)
+__device__ __forceinline__ void planes_fold2(uint32_t (&Z)[8][2], uint32_t x0, uint32_t x1,
+                                             const u32x8& m) {
+  uint32_t pad;  // operand 16 placeholder keeps the body's numbering
+  asm volatile("s_waitcnt lgkmcnt(0)\n\t" PIR_FOLD2_BODY : PIR_FOLD2_Z, "=s"(pad) : PIR_FOLD2_IN);
+  (void)pad;
+}
+#undef PIR_FOLD2_BODY
+#undef PIR_FOLD2_Z
+#undef PIR_FOLD2_IN
+
 __device__ __forceinline__ uint32_t coef_byte(const uint4& c, int a) {
   const uint32_t w = a < 4 ? c.x : (a < 8 ? c.y : (a < 12 ? c.z : c.w));
   return (w >> (8 * (a & 3))) & 0xffu;
@@ -1232,63 +1314,125 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
 #pragma unroll
         for (int v = 0; v < VEC; ++v) Z[a][kk][v] = 0;
     const uint32_t ngroups = (TILE + rpw - 1) / rpw;
-    constexpr int U = SW >= 8 ? 8 : 16;
+    // many rounds, wave-uniform coefficients, 2 dwords per lane: masks from the plane table
+    constexpr bool kPlaneAsm = UNI && VEC == 2 && NQ >= 3;
+    // rows in flight per lane (one record per wave row: a rolling pipeline whose x[] stays live
+    // across tiles; several records per row: U rows loaded, then folded, per batch)
+    constexpr int U = kPlaneAsm ? PIR_PLANE_U : (SW >= 8 ? 8 : 16);
+    // row slot j of a tile = row group wi + j * nwg; rpt slots per tile, a multiple of U (slots
+    // past the tile's row groups are masked)
+    const uint32_t rpt = ((ngroups + nwg - 1) / nwg + U - 1) / U * U;
+    const bool scan = wi < nwg && !(trace && trace_flags_noscan);
     __builtin_amdgcn_s_setprio(2);
     const uint8_t* rbase = shard + (b * region_rows) * pitch + (uint64_t)chunk * CH;
+    // Rolling load pipeline: x[u] holds slot j0 + u; once it is folded, slot j0 + U + u is loaded
+    // into it -- at the end of a tile, from the next tile (of this or the next query).  Shard rows
+    // do not depend on the tree, so U rows per lane stay in flight across tiles and queries; only
+    // the coefficients wait for the tree.
+    Chunk<VEC> x[UNI ? U : 1];
+    // Unconditional loads (straight-line code keeps each refill behind its fold): a slot with
+    // no row reads the shard's first bytes instead, and its coefficient is 0 (or, past the last
+    // tile, it is never folded; inactive lanes' planes are never written out).
+    auto load_slot = [&](uint32_t g, uint32_t j, Chunk<VEC>& dst) __attribute__((always_inline)) {
+      const uint32_t gi = wi + j * nwg;
+      const uint32_t rl = gi * rpw + rec_off;
+      const bool ok = g < total && active && gi < ngroups && rl < TILE;
+      dst = load_chunk<VEC>(ok ? rbase + ((uint64_t)(g & (ntiles - 1)) * TILE + rl) * pitch : shard);
+    };
+    auto fold_row = [&](const Chunk<VEC>& xr, const uint4& c4) __attribute__((always_inline)) {
+#pragma unroll
+      for (int a = 0; a < NQ; ++a) {
+        const uint32_t ca = coef_byte(c4, a);
+        if (UNI && NQ <= 2) {  // scalar branches: ~4 XORs per dword instead of 8 masked
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk)
+            if (ca & (1u << kk)) {
+#pragma unroll
+              for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= xr.v[v];
+            }
+        } else if (UNI) {  // many rounds, 1 dword per lane: branch-free, SGPR masks
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk) {
+            const uint32_t m = 0u - ((ca >> kk) & 1u);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) Z[a][kk][v] = mxor(Z[a][kk][v], xr.v[v], m);
+          }
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk) {
+            const uint32_t m = 0u - ((ca >> kk) & 1u);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= xr.v[v] & m;
+          }
+        }
+      }
+    };
+    if constexpr (UNI) {
+      if (scan) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_slot(0, u, x[u]);
+      }
+    }
     for (uint32_t g = 0; g < total; ++g) {
       const uint32_t i = g % ntiles;
       const uint8_t* ring = sm.ring[g % RING];
       lds_wait_geq(&sm.ready, g + 1);
-      if (wi < nwg && !(trace && trace_flags_noscan)) {
+      if (!UNI && scan) {  // per-lane coefficients: batches of U rows of this tile
         const uint8_t* base = rbase + ((uint64_t)i * TILE) * pitch;
         for (uint32_t g0 = wi; g0 < ngroups; g0 += U * nwg) {
-          Chunk<VEC> x[U];
-          uint4 cf[U];
+          Chunk<VEC> xb[U];
+          uint4 cb[U];
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            const uint32_t gi = g0 + u * nwg;
-            const uint32_t rl = gi * rpw + rec_off;
+            const uint32_t gi = g0 + u * nwg, rl = gi * rpw + rec_off;
             const bool ok = active && gi < ngroups && rl < TILE;
-            if (ok) x[u] = load_chunk<VEC>(base + (uint64_t)rl * pitch);
+            if (ok) xb[u] = load_chunk<VEC>(base + (uint64_t)rl * pitch);
             else
-              for (int v = 0; v < VEC; ++v) x[u].v[v] = 0;
-            if (UNI) {
-              const uint32_t gu = __builtin_amdgcn_readfirstlane(gi);
-              uint4 c4 = gu < ngroups ? load_coef<NRP>(ring, gu) : make_uint4(0, 0, 0, 0);
-              cf[u] = make_uint4(__builtin_amdgcn_readfirstlane(c4.x), __builtin_amdgcn_readfirstlane(c4.y),
-                                 __builtin_amdgcn_readfirstlane(c4.z), __builtin_amdgcn_readfirstlane(c4.w));
-            } else {
-              cf[u] = ok ? load_coef<NRP>(ring, rl) : make_uint4(0, 0, 0, 0);
-            }
+              for (int v = 0; v < VEC; ++v) xb[u].v[v] = 0;
+            cb[u] = ok ? load_coef<NRP>(ring, rl) : make_uint4(0, 0, 0, 0);
           }
 #pragma unroll
-          for (int u = 0; u < U; ++u)
+          for (int u = 0; u < U; ++u) fold_row(xb[u], cb[u]);
+        }
+      }
+      if (UNI && scan) {
+        for (uint32_t j0 = 0; j0 < rpt; j0 += U) {
+          // wave-uniform coefficients: lane u reads row u's (one LDS read), v_readlane broadcasts
+          uint4 cf[U];
+          const uint32_t gl = wi + (j0 + (lane < (uint32_t)U ? lane : 0u)) * nwg;
+          uint4 c4 = load_coef<NRP>(ring, gl < ngroups ? gl : 0u);
+          if (gl >= ngroups) c4 = make_uint4(0, 0, 0, 0);
+          const bool last = j0 + U == rpt;
+          const uint32_t gn = last ? g + 1 : g, jn = last ? 0u : j0 + U;
+          u32x8 mrow;  // kPlaneAsm: masks of the next row's round 0, in flight
+          if constexpr (kPlaneAsm) mrow = plane_masks_issue(__builtin_amdgcn_readlane(c4.x, 0) & 0xffu);
 #pragma unroll
-            for (int a = 0; a < NQ; ++a) {
-              const uint32_t ca = coef_byte(cf[u], a);
-              if (UNI && NQ <= 2) {
+          for (int u = 0; u < U; ++u) {
+            cf[u] = make_uint4(__builtin_amdgcn_readlane(c4.x, u),
+                               NRP > 4 ? __builtin_amdgcn_readlane(c4.y, u) : 0u,
+                               NRP > 8 ? __builtin_amdgcn_readlane(c4.z, u) : 0u,
+                               NRP > 8 ? __builtin_amdgcn_readlane(c4.w, u) : 0u);
+            if constexpr (kPlaneAsm) {
+              u32x8 m = mrow;
 #pragma unroll
-                for (int kk = 0; kk < 8; ++kk)
-                  if (ca & (1u << kk)) {
-#pragma unroll
-                    for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= x[u].v[v];
-                  }
-              } else if (UNI) {
-#pragma unroll
-                for (int kk = 0; kk < 8; ++kk) {
-                  const uint32_t m = 0u - ((ca >> kk) & 1u);
-#pragma unroll
-                  for (int v = 0; v < VEC; ++v) Z[a][kk][v] = mxor(Z[a][kk][v], x[u].v[v], m);
-                }
-              } else {
-#pragma unroll
-                for (int kk = 0; kk < 8; ++kk) {
-                  const uint32_t m = 0u - ((ca >> kk) & 1u);
-#pragma unroll
-                  for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= x[u].v[v] & m;
-                }
+              for (int a = 0; a < NQ; ++a) {
+                auto& Za = reinterpret_cast<uint32_t(&)[8][2]>(Z[a]);
+                if (a + 1 < NQ)
+                  m = planes_fold2_next(Za, x[u].v[0], x[u].v[VEC - 1], m, coef_byte(cf[u], a + 1));
+                else if (u + 1 < U)
+                  mrow = planes_fold2_next(Za, x[u].v[0], x[u].v[VEC - 1], m,
+                                           __builtin_amdgcn_readlane(c4.x, u + 1) & 0xffu);
+                else
+                  planes_fold2(Za, x[u].v[0], x[u].v[VEC - 1], m);
               }
+            } else {
+              fold_row(x[u], cf[u]);
             }
+            load_slot(gn, jn + u, x[u]);
+            // keep the refill behind its fold: x[u]'s registers are reused (no second buffer),
+            // and the wait before the next fold is vmcnt(U - 1), not a drain
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
       }
       lds_signal(&sm.consumed[g % RING]);
@@ -1700,6 +1844,9 @@ hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_
                         uint64_t* trace) {
   if (nk < 1 || (qp.ls && !scratch)) return hipErrorInvalidValue;
 #define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, scratch, s, trace)
+#ifdef PIR_DEV_NQ  // development builds only (ISA / register checks): one round count
+  return qp.shape.nq == PIR_DEV_NQ && qp.tile == 1024 ? PIR_Q(PIR_DEV_NQ, 1024) : hipErrorInvalidValue;
+#else
   if (qp.tile == 4096) {
     switch (qp.shape.nq) {
       case 1: return PIR_Q(1, 4096);
@@ -1719,6 +1866,7 @@ hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_
     case 8: return PIR_Q(8, 1024);
     default: return hipErrorInvalidValue;
   }
+#endif
 #undef PIR_Q
 }
 
