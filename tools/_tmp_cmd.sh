@@ -1,6 +1,11 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 300 python -m pytest tests/test_gpu_batch.py -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-for B in 1 2; do for G in 8 16; do PIR_BATCH_SCAN_BPC=$B PIR_BATCH_G=$G timeout -k 10 300 python bench.py --config c3b --steps 2 --warmup 1 > gpurun_out/c3b_g$G.log 2>&1 || exit $?; echo "bpc=$B G=$G"; tail -1 gpurun_out/c3b_g$G.log | cut -c 180-300; done; done
-rm -rf gpurun_out/prof_c3b
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3b -o run --output-format csv -- python bench.py --config c3b --steps 1 --warmup 1 > gpurun_out/prof_c3b.log 2>&1; echo rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || exit $?
+tail -1 gpurun_out/smoke.log
+timeout -k 10 300 python bench.py > gpurun_out/bench_default.log 2>&1 || exit $?
+tail -1 gpurun_out/bench_default.log | cut -c 1-400
+for c in c5 c24 c3; do
+  timeout -k 10 300 python bench.py --config $c --steps 20 --warmup 5 --no-cpu > gpurun_out/bench_$c.log 2>&1 || exit $?
+  python -c "import json,sys; d=json.loads(open('gpurun_out/bench_$c.log').read().strip().splitlines()[-1]); print('$c', d['value'], d['ms_per_step'], d.get('roofline',{}).get('frac'))"
+done
