@@ -78,6 +78,7 @@ PROTOTYPES = {
     "pir_engine_answer_batch_dev": (_I, [_P, _P, _I, _P, _P]),
     "pir_engine_answer_batch": (_I, [_P, _P, _I, _P]),
     "pir_engine_answer_stream_dev": (_I, [_P, _P, _I, _P, _P]),
+    "pir_engine_reserve_queue": (_I, [_P, _I]),
     "pir_engine_set_batch_group": (_I, [_P, _I]),
     "pir_engine_batch_group": (_I, [_P]),
     "pir_engine_stream": (_P, [_P]),

@@ -812,6 +812,25 @@ int pir_engine_answer_stream_dev(pir_engine_t* e, const uint8_t* d_keys, int num
   return answer_stream_locked(e, d_keys, num_keys, d_result, s);
 }
 
+int pir_engine_reserve_queue(pir_engine_t* e, int num_keys) {
+  if (!e || num_keys < 1) return fail(PIR_EINVAL, "bad argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const auto& c = e->cfg;
+  const pir::QueryPlan qp = pir::make_query_plan(c.log_num_records, c.log_num_partitions,
+                                                 c.num_parties, c.num_rounds, e->pitch, e->num_cus,
+                                                 num_keys);
+  if (!qp.tile) return PIR_OK;  // shapes k_query does not take allocate per answer
+  int rc = ensure_slabs(e, (size_t)num_keys * pir::query_slab_bytes(qp));
+  if (!rc) rc = ensure_buf(&e->d_qscratch, &e->qscratch_cap, pir::query_scratch_bytes(qp));
+  if (!rc && e->comm) {
+    const size_t total = (size_t)num_keys * c.num_rounds * c.record_bytes;
+    rc = ensure_buf(&e->d_bpart, &e->bpart_cap, total);
+    if (!rc) rc = ensure_buf(&e->d_bgather, &e->bgather_cap, total * e->nranks);
+  }
+  return rc;
+}
+
 int pir_engine_set_batch_group(pir_engine_t* e, int keys_per_pass) {
   if (!e || keys_per_pass < 0 || keys_per_pass > 16) return fail(PIR_EINVAL, "bad argument");
   e->batch_group = keys_per_pass;

@@ -190,6 +190,11 @@ class Engine:
         check(self._lib.pir_engine_answer_stream_dev(self._h, d_keys, num_keys, d_result, stream),
               "answer_stream_dev")
 
+    def reserve_queue(self, num_keys):
+        """Pre-size the work buffers for queues of up to num_keys queries (no allocation, and
+        so no device synchronisation, inside later answer_stream_dev calls)."""
+        check(self._lib.pir_engine_reserve_queue(self._h, num_keys), "reserve_queue")
+
     def answer_stream(self, keys):
         """Host form of answer_stream_dev: [num_keys, num_rounds, record_bytes]."""
         keys = [bytes(k) for k in keys]

@@ -107,6 +107,10 @@ int pir_engine_answer_batch(pir_engine_t *e, const uint8_t *keys, int num_keys,
  * the shape allows, so that the tree of query k+1 is built while query k's rows stream. */
 int pir_engine_answer_stream_dev(pir_engine_t *e, const uint8_t *d_keys, int num_keys,
                                  uint8_t *d_result, void *stream);
+/* pre-size the device work buffers of pir_engine_answer_stream_dev for queues of up to
+ * `num_keys` queries (a server sizes its queue at setup), so that no answer call allocates:
+ * the reference has no counterpart (its buffers are host mallocs per call, server.cpp:108-114). */
+int pir_engine_reserve_queue(pir_engine_t *e, int num_keys);
 /* keys per shard pass: 0 = automatic (8 / nrp), else a power of two <= 16 / nrp, where nrp =
  * num_rounds rounded up to a power of two.  Default from $PIR_BATCH_G. */
 int pir_engine_set_batch_group(pir_engine_t *e, int keys_per_pass);

@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <thread>
 #include <vector>
 
 #include "utils.h"
@@ -153,6 +154,35 @@ double ref_server_time(void* hv, const uint8_t* key, uint8_t* result, int reps) 
     for (int r = 0; r < reps; r++) ref_server_answer(hv, key, result);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}
+
+// All-cores aggregate: `nthreads` independent runOptimizedDPFTreeQuery
+// calls at once, one per thread.  Each thread gets a shallow copy of the server whose only
+// private member is its EVP context (the reference's ctx is not shareable); the shard rows
+// are shared read-only.  Returns the wall-clock seconds until the last query finishes.
+double ref_server_time_parallel(void* hv, const uint8_t* key, uint8_t* result, int nthreads) {
+    ref_srv* h = (ref_srv*)hv;
+    set_tree_globals(h->p, h->n, h->efs, h->nq);
+    std::vector<server> views(nthreads, h->s);
+    std::vector<std::vector<uint8_t>> outs(nthreads, std::vector<uint8_t>((size_t)h->nq * h->efs));
+    for (auto& v : views) v.ctx = EVP_CIPHER_CTX_new();
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    std::vector<std::thread> th;
+    for (int i = 0; i < nthreads; i++)
+        th.emplace_back([&, i] {
+            std::vector<uint8_t*> res(h->nq);
+            for (int a = 0; a < h->nq; a++) res[a] = outs[i].data() + (size_t)a * h->efs;
+            runOptimizedDPFTreeQuery(&views[i], (uint8_t*)key, h->nq, res.data());
+        });
+    for (auto& t : th) t.join();
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    for (auto& v : views) EVP_CIPHER_CTX_free(v.ctx);
+    memcpy(result, outs[0].data(), outs[0].size());
+    int same = 1;
+    for (int i = 1; i < nthreads; i++) same &= outs[i] == outs[0];
+    double dt = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+    return same ? dt : -dt;
 }
 
 // params.cpp:467-642 sizing for tree mode: setSystemParams(L,f,t=1,k,r,b=0,rho,mac,mode=0)
