@@ -126,6 +126,20 @@ __device__ __forceinline__ void aes_ctr_row(const Tab& T, uint4 key, uint4 (&out
   for (int r = 0; r < 9; ++r) {
     key_next(T, k0, k1, k2, k3, kRcon[r]);
     const uint32_t r0 = rotr8(k0), r1 = rotr8(k1), r2 = rotr8(k2), r3 = rotr8(k3);
+    if (r == 0) {
+      // first round: the blocks differ only in byte 15 (the counter), which only output column
+      // 0 reads (T.t2<3>(w3) in round_row), so columns 1-3 are block 0's for every block
+#pragma unroll
+      for (int b = 1; b < NB; ++b)
+        w[b][0] = xor3(T.t0<0>(w[b][0]), T.t2<2>(w[b][2]),
+                       rotl8(xor3(T.t0<1>(w[b][1]), T.t2<3>(w[b][3]), r0)));
+      round_row(T, w[0][0], w[0][1], w[0][2], w[0][3], r0, r1, r2, r3);
+#pragma unroll
+      for (int b = 1; b < NB; ++b) {
+        w[b][1] = w[0][1]; w[b][2] = w[0][2]; w[b][3] = w[0][3];
+      }
+      continue;
+    }
 #pragma unroll
     for (int b = 0; b < NB; ++b) round_row(T, w[b][0], w[b][1], w[b][2], w[b][3], r0, r1, r2, r3);
   }
