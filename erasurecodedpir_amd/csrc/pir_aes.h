@@ -129,6 +129,7 @@ __device__ __forceinline__ void aes_ctr_row(const Tab& T, uint4 key, uint4 (&out
     if (r == 0) {
       // first round: the blocks differ only in byte 15 (the counter), which only output column
       // 0 reads (T.t2<3>(w3) in round_row), so columns 1-3 are block 0's for every block
+      // (NB = 1 costs the same as round_row in this and the next round)
 #pragma unroll
       for (int b = 1; b < NB; ++b)
         w[b][0] = xor3(T.t0<0>(w[b][0]), T.t2<2>(w[b][2]),
@@ -137,6 +138,25 @@ __device__ __forceinline__ void aes_ctr_row(const Tab& T, uint4 key, uint4 (&out
 #pragma unroll
       for (int b = 1; b < NB; ++b) {
         w[b][1] = w[0][1]; w[b][2] = w[0][2]; w[b][3] = w[0][3];
+      }
+      continue;
+    }
+    if (r == 1) {
+      // second round: the blocks still share columns 1-3, so each output column is three
+      // lookups of the shared columns (once) plus one of the block's own column 0 (rotl8 is
+      // linear over XOR, so the column-0 term can leave round_row's rotl8)
+      const uint32_t a1 = w[0][1], a2 = w[0][2], a3 = w[0][3];
+      const uint32_t s0 = T.t2<2>(a2) ^ rotl8(xor3(T.t0<1>(a1), T.t2<3>(a3), r0));
+      const uint32_t s1 = xor3(T.t0<0>(a1), T.t2<2>(a3), rotl8(T.t0<1>(a2) ^ r1));
+      const uint32_t s2 = T.t0<0>(a2) ^ rotl8(xor3(T.t0<1>(a3), T.t2<3>(a1), r2));
+      const uint32_t s3 = xor3(T.t0<0>(a3), T.t2<2>(a1), rotl8(T.t2<3>(a2) ^ r3));
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const uint32_t x = w[b][0];
+        w[b][0] = T.t0<0>(x) ^ s0;
+        w[b][1] = s1 ^ rotl8(T.t2<3>(x));
+        w[b][2] = s2 ^ T.t2<2>(x);
+        w[b][3] = s3 ^ rotl8(T.t0<1>(x));
       }
       continue;
     }
