@@ -77,7 +77,10 @@ def cpu_baseline(keys_party1, shard_rows, n, efs, p, nq, gpu_answer, budget_s=20
         reps = max(1, min(8, int(budget_s / max(t1, 1e-3)) - 1))
         t = L.ref_server_time(ctypes.c_void_p(h), P(keyb), P(res), reps) if reps else t1
         # all-cores aggregate: one independent query per core at once
-        all_cores = _cpu_all_cores(shard_rows, keyb, n, efs, p, nq, res)
+        try:
+            all_cores = _cpu_all_cores(shard_rows, keyb, n, efs, p, nq, res)
+        except (OSError, RuntimeError, ValueError) as exc:  # a reported baseline: never fatal
+            all_cores = {"error": f"{type(exc).__name__}: {exc}"}
         L.ref_server_free(ctypes.c_void_p(h))
         kind, src = "reference", "oracle/_ref/libref.so: reference src/c runOptimizedDPFTreeQuery (OpenSSL EVP AES, log/exp gf_mul)"
     else:
@@ -117,7 +120,13 @@ def _cpu_all_cores(shard_rows, keyb, n, efs, p, nq, ref_answer):
     shard_bytes = (1 << n) * efs
     if ncores * shard_bytes > (64 << 30):  # each worker copies the shard into its own rows
         ncores = max(1, (64 << 30) // shard_bytes)
-    path = f"/dev/shm/pir_bench_cpu_{os.getpid()}.bin"
+    import tempfile
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
+    if shm:
+        st = os.statvfs(shm)
+        if st.f_bavail * st.f_frsize < shard_bytes + (256 << 20):
+            shm = None
+    path = os.path.join(shm or tempfile.gettempdir(), f"pir_bench_cpu_{os.getpid()}.bin")
     np.ascontiguousarray(shard_rows).reshape(-1).tofile(path)
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", path, str(n), str(efs),
            str(p), str(nq), keyb.tobytes().hex()]
