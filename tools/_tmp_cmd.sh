@@ -1,3 +1,5 @@
+# GPU session (through tools/gpu.sh): the round-end checks the driver runs -- GPU test suite,
+# smoke, default bench -- each step under its own time limit; the first failure ends the call.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
