@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X tree-DPF PIR answer path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c24|c3|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c24|c2|c3|c5|c4|c3b]
 
 A step = one PIR query answered against the device-resident shard: key parse -> DPF
 full-domain evaluation (AES-128 PRG tree) -> GF(2^8) inner product over every record ->
@@ -9,26 +9,36 @@ partial-answer reduce (-> RCCL all-gather + XOR fold across GPUs when N > 1).  I
 keys) are resident in HBM before the timed region; the answers stay in HBM.  The K timed steps
 are K independent queries (distinct keys) answered as a queue: one launch of the query kernel,
 each query still its own tree and its own full shard pass, the tree of query k+1 built while
-query k's rows stream.  The same K queries answered one launch at a time are reported as
-`single_query` (the per-query latency).
+query k's rows stream.  W warm-up queries (a queue of W) run before it.  The same K queries
+answered one launch at a time are reported as `single_query` (the per-query latency).
 
-N = 1: BASELINE configs[1] ("c2"): one shard of 2^20 x 1 KiB, DPF depth 20, batch = 1 query.
-N > 1: the split-shard layout (configs[3]'s structure), weak scaling: every GPU holds a 2^20 x
-1 KiB partition of one logical 2^(20+log2 N)-record shard; rank r evaluates the DPF subtree of
-its partition and the partial answers are XOR-all-reduced over RCCL.  `value` = logical shard
-bytes / time per query (whole job).  Launched per the driver contract with
-torch.distributed.run (gloo carries the barrier / timing max / RCCL unique id).
+Workloads:
+  N = 1, default "c24": the north_star target shape, one shard of 2^24 x 1 KiB (16 GiB),
+         p = 2.  The same line carries configs[1] (2^20 x 1 KiB, batch = 1) as `configs1_c2`
+         and the N = 1 point of the split-shard curve (the 2^27 x 1 KiB logical shard as one
+         128 GiB engine) as `c4_single_engine`.
+  N > 1, default "c4": BASELINE configs[3], one logical server of 2^27 x 1 KiB split over the
+         N GPUs (strong scaling: rank r holds rows [r 2^27/N, (r+1) 2^27/N) and evaluates the DPF
+         subtree of its partition); the partial answers are combined by ONE RCCL all-gather +
+         XOR fold per queue.  Rank 0 then answers the same queries with the whole shard on its
+         own GPU (`n1_reference`), so the line carries the speedup over one GPU.
+  --config c2|c3|c5 at N > 1: weak scaling (2^n rows per GPU of a 2^(n + log2 N) logical shard).
+Launched per the driver contract with torch.distributed.run (gloo carries the barrier, the
+timing max and the RCCL unique id).
 
 rank 0 also prints the roofline of the dominant kernel (k_query: algorithmic bytes = K x
-records x record_bytes per launch, HIP-event duration of the launch) and a
-CPU baseline: the reference src/c (oracle/_ref/libref.so, compiled from the reference's own
-sources) -- or the oracle restatement if that is absent -- timed on this host on a bounded
-sample of the same workload; the CPU answer is also checked against the GPU answer bit-exactly.
+records x record_bytes per launch over the HIP-event duration of that launch) and a CPU
+baseline: the reference src/c (oracle/_ref/libref.so, compiled from the reference's own
+sources) on one host core answering one query of the SAME workload at full size, checked
+bit-exactly against the GPU answer, plus an all-cores aggregate (one reference process per
+core over one shared copy of the shard).
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -39,13 +49,16 @@ sys.path.insert(0, ROOT)
 METRIC = "device-resident shard GiB/s per PIR query, 1/2/4/8 MI355X; bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
 GIB = float(1 << 30)
+SHARD_SEED = 0xC0FFEE
 
 CONFIGS = {
-    # name: (log records per GPU, record bytes, parties, rounds, workload text)
-    "c2": (20, 1024, 2, 1, "configs[1]: 1 MI355X, one shard 2^20 x 1 KiB, DPF depth 20, batch=1 query"),
-    "c24": (24, 1024, 2, 1, "north_star target shape: one shard 2^24 x 1 KiB, DPF depth 24, 1 query"),
-    "c3": (24, 256, 2, 1, "configs[2] shape per query: one shard 2^24 x 256 B (queries answered one at a time)"),
-    "c5": (24, 1024, 8, 5, "configs[4] per-GPU server: 2^24 x 1 KiB shard, p=8 (k=5, r=2), NUM_ROUNDS=5"),
+    # name: (log records, record bytes, parties, rounds, strong, workload text)
+    # strong=False: 2^n rows per GPU (weak scaling); strong=True: 2^n rows in all
+    "c24": (24, 1024, 2, 1, False, "north_star target shape: one shard 2^24 x 1 KiB, DPF depth 24, p=2"),
+    "c2": (20, 1024, 2, 1, False, "configs[1]: 1 MI355X, one shard 2^20 x 1 KiB, DPF depth 20, batch=1 query"),
+    "c3": (24, 256, 2, 1, False, "configs[2] shape per query: one shard 2^24 x 256 B (queries answered one at a time)"),
+    "c5": (24, 1024, 8, 5, False, "configs[4] per-GPU server: 2^24 x 1 KiB shard, p=8 (k=5, r=2), NUM_ROUNDS=5"),
+    "c4": (27, 1024, 2, 1, True, "configs[3]: one logical server, 2^27 x 1 KiB split over the GPUs, RCCL all-gather + XOR fold"),
 }
 # batched configs: a step answers `batch` keys (distinct indices) against the shard
 BATCH_CONFIGS = {
@@ -60,74 +73,97 @@ def dist_env():
     return world, rank, local
 
 
-def cpu_baseline(keys_party1, shard_rows, n, efs, p, nq, gpu_answer, budget_s=20.0):
-    """Time the reference CPU path (runOptimizedDPFTreeQuery) on one core of this host."""
-    import ctypes
+# ------------------------------------------------------------------------------- CPU baseline
+def _ref_lib():
+    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libref.so"))
+    L.ref_server_view.restype = ctypes.c_void_p
+    L.ref_server_view.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p]
+    L.ref_server_view_free.argtypes = [ctypes.c_void_p]
+    L.ref_server_time.restype = ctypes.c_double
+    L.ref_server_time.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    return L
+
+
+def dump_shard(eng, path, chunk_rows=1 << 20):
+    """The engine's rows -> a host file, in chunks (no full-size host copy)."""
+    with open(path, "wb") as f:
+        for r0 in range(0, eng.num_rows, chunk_rows):
+            eng.get_shard(r0, min(chunk_rows, eng.num_rows - r0)).tofile(f)
+
+
+def shard_file_path(nbytes):
+    """A file for the shard copy the CPU processes share: /dev/shm when it has room."""
+    d = "/dev/shm"
+    if not (os.path.isdir(d) and os.access(d, os.W_OK)):
+        d = None
+    else:
+        st = os.statvfs(d)
+        if st.f_bavail * st.f_frsize < nbytes + (1 << 30):
+            d = None
+    return os.path.join(d or tempfile.gettempdir(), f"pir_bench_shard_{os.getpid()}.bin")
+
+
+def cpu_baseline(path, n, efs, p, nq, key, gpu_answer, budget_s, cores):
+    """The reference runOptimizedDPFTreeQuery (oracle/_ref/libref.so) on this host over the same
+    shard (a read-only mapping of `path`): one core, then `cores` processes at once."""
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libref.so")
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    if not os.path.exists(ref_so):
+        return _cpu_port(path, n, efs, p, nq, key, gpu_answer)
+    L = _ref_lib()
+    shard = np.memmap(path, np.uint8, mode="r")
+    keyb = np.frombuffer(bytes(key), np.uint8).copy()
     res = np.zeros(nq * efs, np.uint8)
-    keyb = np.frombuffer(keys_party1, np.uint8).copy()
     P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-    if os.path.exists(ref_so):
-        L = ctypes.CDLL(ref_so)
-        L.ref_server_new.restype = ctypes.c_void_p
-        L.ref_server_time.restype = ctypes.c_double
-        h = L.ref_server_new(p, 1, n, efs, nq, P(shard_rows), 0, 1)
-        t1 = L.ref_server_time(ctypes.c_void_p(h), P(keyb), P(res), 1)
-        reps = max(1, min(8, int(budget_s / max(t1, 1e-3)) - 1))
-        t = L.ref_server_time(ctypes.c_void_p(h), P(keyb), P(res), reps) if reps else t1
-        # all-cores aggregate (SURVEY.md 8(d)): one independent query per core at once
+    h = L.ref_server_view(p, 1, n, efs, nq, P(shard))
+    t1 = L.ref_server_time(h, P(keyb), P(res), 1)
+    reps = max(0, min(8, int(budget_s / max(t1, 1e-3)) - 1))  # first call doubles as warm-up
+    t = L.ref_server_time(h, P(keyb), P(res), reps) / reps if reps else t1
+    L.ref_server_view_free(h)
+    del shard
+    parity = bool(np.array_equal(res.reshape(nq, efs), gpu_answer))
+    all_cores = None
+    if cores > 1:
         try:
-            all_cores = _cpu_all_cores(shard_rows, keyb, n, efs, p, nq, res)
+            all_cores = _cpu_all_cores(path, keyb, n, efs, p, nq, res, cores)
         except (OSError, RuntimeError, ValueError) as exc:  # a reported baseline: never fatal
             all_cores = {"error": f"{type(exc).__name__}: {exc}"}
-        L.ref_server_free(ctypes.c_void_p(h))
-        kind, src = "reference", "oracle/_ref/libref.so: reference src/c runOptimizedDPFTreeQuery (OpenSSL EVP AES, log/exp gf_mul)"
-    else:
-        import _oracle as O
-        t0 = time.perf_counter()
-        res = O.answer(p, 1, n, efs, nq, keys_party1, shard_rows).reshape(-1)
-        t1 = time.perf_counter() - t0
-        reps, t = 1, t1
-        all_cores = None
-        kind, src = "port", "oracle/liboracle.so: plain-C restatement (single thread)"
-    per_query = t / max(reps, 1)
-    parity = bool(np.array_equal(res.reshape(nq, efs), gpu_answer))
     return {
-        "value": ((1 << n) * efs / GIB) / per_query,
+        "value": ((1 << n) * efs / GIB) / t,
         "unit": "GiB/s",
         "cores": 1,
-        "kind": kind,
-        "sample": f"{max(reps,1)} + 1 warm-up queries of the same workload (2^{n} x {efs} B, p={p}, "
-                  f"NUM_ROUNDS={nq}) on 1 host core; {per_query:.3f} s/query; {src}",
-        "s_per_query": per_query,
+        "kind": "reference",
+        "sample": f"{1 + reps} queries of the same workload at full size (2^{n} x {efs} B, p={p}, "
+                  f"NUM_ROUNDS={nq}) on 1 host core, {t:.3f} s per query"
+                  + (" (the first one timed)" if not reps else " (first one untimed)")
+                  + "; oracle/_ref/libref.so: the reference src/c runOptimizedDPFTreeQuery "
+                    "(OpenSSL EVP AES, log/exp gf_mul) over indexList rows pointing into a "
+                    "read-only mapping of the shard",
+        "s_per_query": t,
         "bit_exact_vs_gpu": parity,
         "host_cpu": _cpu_model(),
         "all_cores": all_cores,
     }
 
 
-def _cpu_all_cores(shard_rows, keyb, n, efs, p, nq, ref_answer):
-    """All-cores reference aggregate: C worker PROCESSES (one per core of this process's CPU
-    share), each holding its own reference server over the same shard and answering one query,
-    started together.  Processes, not threads: in one process the reference's per-node
-    EVP_EncryptInit_ex (utils.cpp:42) serialises on OpenSSL 3's shared cipher-fetch locks
-    (measured: 16 threads answer no faster than 1)."""
+def _cpu_port(path, n, efs, p, nq, key, gpu_answer):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    shard = np.memmap(path, np.uint8, mode="r")
+    t0 = time.perf_counter()
+    res = O.answer(p, 1, n, efs, nq, key, shard)
+    t = time.perf_counter() - t0
+    return {"value": ((1 << n) * efs / GIB) / t, "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"1 query at full size on 1 host core; oracle/liboracle.so (plain-C "
+                      f"restatement); {t:.3f} s", "s_per_query": t,
+            "bit_exact_vs_gpu": bool(np.array_equal(res, gpu_answer)), "host_cpu": _cpu_model()}
+
+
+def _cpu_all_cores(path, keyb, n, efs, p, nq, ref_answer, ncores):
+    """All-cores reference aggregate: `ncores` worker PROCESSES, each a reference server over
+    the same read-only shard mapping answering one query, started together.  Processes, not
+    threads: in one process the reference's per-node EVP_EncryptInit_ex (utils.cpp:42)
+    serialises on OpenSSL 3's shared cipher-fetch locks (16 threads answer no faster than 1)."""
     import subprocess
-    # at most 15 workers: with this (GPU) process that keeps within the GPU box's 16-process
-    # guard even while a freshly forked child still holds the parent's device handle
-    ncores = min(_host_cores(), 15)
-    shard_bytes = (1 << n) * efs
-    if ncores * shard_bytes > (64 << 30):  # each worker copies the shard into its own rows
-        ncores = max(1, (64 << 30) // shard_bytes)
-    import tempfile
-    shm = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
-    if shm:
-        st = os.statvfs(shm)
-        if st.f_bavail * st.f_frsize < shard_bytes + (256 << 20):
-            shm = None
-    path = os.path.join(shm or tempfile.gettempdir(), f"pir_bench_cpu_{os.getpid()}.bin")
-    np.ascontiguousarray(shard_rows).reshape(-1).tofile(path)
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", path, str(n), str(efs),
            str(p), str(nq), keyb.tobytes().hex()]
     procs = []
@@ -137,7 +173,6 @@ def _cpu_all_cores(shard_rows, keyb, n, efs, p, nq, ref_answer):
         for pr in procs:
             if pr.stdout.readline().strip() != "ready":
                 raise RuntimeError("cpu worker failed to start")
-        os.unlink(path)
         t0 = time.perf_counter()
         for pr in procs:
             pr.stdin.write("go\n")
@@ -149,14 +184,14 @@ def _cpu_all_cores(shard_rows, keyb, n, efs, p, nq, ref_answer):
             if pr.poll() is None:
                 pr.kill()
             pr.wait()
-        if os.path.exists(path):
-            os.unlink(path)
     agree = all(len(o) == 2 and o[1] == ref_answer.tobytes().hex() for o in outs)
     per = [float(o[0]) for o in outs if o]
+    shard_bytes = (1 << n) * efs
     return {
         "value": ncores * (shard_bytes / GIB) / wall, "unit": "GiB/s", "cores": ncores,
-        "sample": f"{ncores} worker processes, one query each, started together: {wall:.3f} s wall "
-                  f"(per-process {min(per):.3f}-{max(per):.3f} s)",
+        "sample": f"{ncores} worker processes over one shared read-only copy of the shard, one "
+                  f"full-size query each, started together: {wall:.3f} s wall (per-process "
+                  f"{min(per):.3f}-{max(per):.3f} s)",
         "answers_agree": bool(agree),
     }
 
@@ -164,30 +199,27 @@ def _cpu_all_cores(shard_rows, keyb, n, efs, p, nq, ref_answer):
 def _cpu_worker(argv):
     """Child of _cpu_all_cores (never touches the GPU): a reference server over the shared shard
     file, one runOptimizedDPFTreeQuery on "go"; prints seconds and the answer hex."""
-    import ctypes
     path, n, efs, p, nq, keyhex = argv[0], *map(int, argv[1:5]), argv[5]
-    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libref.so"))
-    L.ref_server_new.restype = ctypes.c_void_p
-    L.ref_server_time.restype = ctypes.c_double
-    shard = np.fromfile(path, np.uint8)
+    L = _ref_lib()
+    shard = np.memmap(path, np.uint8, mode="r")
     key = np.frombuffer(bytes.fromhex(keyhex), np.uint8).copy()
     res = np.zeros(nq * efs, np.uint8)
     P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-    h = L.ref_server_new(p, 1, n, efs, nq, P(shard), 0, 1)
-    del shard
+    h = L.ref_server_view(p, 1, n, efs, nq, P(shard))
     print("ready", flush=True)
     sys.stdin.readline()
-    t = L.ref_server_time(ctypes.c_void_p(h), P(key), P(res), 1)
+    t = L.ref_server_time(h, P(key), P(res), 1)
     print(f"{t:.6f} {res.tobytes().hex()}", flush=True)
-    L.ref_server_free(ctypes.c_void_p(h))
+    L.ref_server_view_free(h)
 
 
 def _host_cores():
-    """Host threads for the all-cores CPU leg: this process's CPU share (the GPU box grants
-    16 per GPU; nproc there shows the whole machine), capped by the affinity mask."""
+    """Host processes for the all-cores CPU leg: this process's CPU share (the GPU box grants
+    16 per GPU; nproc there shows the whole machine), capped by the affinity mask; one core is
+    left to this (GPU) process, which also keeps within the box's 16-process guard."""
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     aff = len(os.sched_getaffinity(0))
-    return max(1, min(share, aff) if share > 0 else min(aff, 16))
+    return max(1, (min(share, aff) if share > 0 else min(aff, 16)) - 1)
 
 
 def _cpu_model():
@@ -200,25 +232,176 @@ def _cpu_model():
     return "unknown"
 
 
+# --------------------------------------------------------------------------------- GPU legs
+def _gf_table(c):
+    t = np.zeros(256, np.uint8)
+    for x in range(256):
+        a, b, r = c, x, 0
+        while b:
+            if b & 1:
+                r ^= a
+            a = ((a << 1) ^ (0x11D if a & 0x80 else 0)) & 0xFF
+            b >>= 1
+        t[x] = r
+    return t
+
+
+class Ctx:
+    """Distributed context: barrier + device sync around timed regions, max over ranks."""
+
+    def __init__(self, world, rank, local):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world, self.rank, self.local = world, rank, local
+
+    def timed(self, eng, fn):
+        self.sync(eng)
+        t0 = time.perf_counter()
+        fn()
+        self.sync(eng)
+        dt = time.perf_counter() - t0
+        if self.world > 1:
+            tt = self.torch.tensor([dt], dtype=self.torch.float64)
+            self.dist.all_reduce(tt, op=self.dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        return dt
+
+    def sync(self, eng):
+        eng.sync()
+        self.torch.cuda.synchronize()
+        if self.world > 1:
+            self.dist.barrier()
+
+
+def make_keys(pir, n, p, nq, count, rng, device, first=None):
+    """count independent queries (distinct indices): [(index, [key of party 1, ..., p])]."""
+    idxs = [int(i) for i in rng.choice(1 << n, count, replace=False)]
+    if first is not None:
+        idxs[0] = first
+    fcw = pir.final_cw(p, nq, 1)
+    return [(i, pir.gen_keys(n, i, p, nq, fcw=fcw,
+                             seeds=rng.integers(0, 256, 16 * p, dtype=np.uint8).tobytes(),
+                             device=device)) for i in idxs], fcw
+
+
+def measure(ctx, eng, keys, W, K, single=True):
+    """Warm-up queue of W, then the timed queue of K (HIP events around the query kernel), then
+    the same K queries one launch each.  keys: party-1 keys (W + K of them)."""
+    kl, ab = eng.key_len, eng.answer_bytes
+    nkeys = W + K
+    d_keys = eng.alloc_dev(kl * nkeys)
+    d_res = eng.alloc_dev(ab * nkeys)
+    eng.h2d(d_keys, b"".join(keys))
+    d_kq, d_rq = d_keys + W * kl, d_res + W * ab
+    eng.reserve_queue(max(W, K, 1))  # queue buffers sized at setup, as a server would
+    if W:
+        eng.answer_stream_dev(d_keys, W, d_res)
+    eng.set_profiling(1)
+    dt = ctx.timed(eng, lambda: eng.answer_stream_dev(d_kq, K, d_rq))
+    phases = eng.last_timings()
+    eng.set_profiling(0)
+    queue = eng.d2h(d_rq, ab * K).reshape(K, eng.num_rounds, eng.record_bytes)
+    out = {"ms": dt / K * 1e3, "phases": phases, "answers": queue}
+    if single:
+        for i in range(max(1, min(W, 5))):  # warm the one-query kernel (its own code object)
+            eng.answer_dev(d_keys + (i % nkeys) * kl, d_res + (i % nkeys) * ab)
+        dt1 = ctx.timed(eng, lambda: [eng.answer_dev(d_kq + i * kl, d_rq + i * ab)
+                                      for i in range(K)])
+        singles = eng.d2h(d_rq, ab * K).reshape(K, eng.num_rounds, eng.record_bytes)
+        eng.set_profiling(max(K, 1))
+        for i in range(K):
+            eng.answer_dev(d_kq + i * kl, d_rq + i * ab)
+        out.update(ms1=dt1 / K * 1e3, phases1=eng.last_timings(), singles=singles)
+        eng.set_profiling(0)
+    eng.free_dev(d_keys)
+    eng.free_dev(d_res)
+    return out
+
+
+def pir_check(ctx, eng, keyset, fcw, q_answers, n, g):
+    """Full-size PIR property on every rank: the party-1 answers (from the queue) XOR the
+    party-2 answers of the same queries == finalCW * record (p = 2, one round)."""
+    import erasurecodedpir_amd as pir  # noqa: F401
+    tab = _gf_table(int(fcw[0]))
+    eng.set_party(2)
+    ok = True
+    for q, (idx, ks) in enumerate(keyset):
+        a2 = eng.answer(ks[1])
+        owner = idx >> (n - g) if g else 0
+        rec = eng.shard_row(idx - owner * eng.num_rows) if ctx.rank == owner else None
+        if ctx.world > 1:
+            rec = broadcast_from(rec, owner, eng.record_bytes)
+        ok &= bool(np.array_equal(q_answers[q][0] ^ a2[0], tab[rec]))
+    eng.set_party(1)
+    return ok
+
+
+def roofline(kern_ms, local_bytes, K, config, world):
+    algo = local_bytes * K
+    achieved = algo / (kern_ms / 1e3) / 1e9 if kern_ms == kern_ms and kern_ms > 0 else None
+    traffic, src = _pmc_traffic(config, world, K)
+    return {
+        "bound": "hbm",
+        "kernel": f"k_query (DPF tree + GF(2^8) shard scan, {K} queries per launch)",
+        "achieved": round(achieved, 1) if achieved else None,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+        "traffic": traffic,
+        "traffic_source": src,
+        "algorithmic_bytes_per_launch": int(algo),
+        "algorithmic_bytes_per_query": int(local_bytes),
+        "kernel_ms_per_launch": round(kern_ms, 5),
+    }
+
+
+def _pmc_traffic(config, world, queries_per_launch):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc passes
+    (profiles/pmc_<config>.json: bytes per query, measured), scaled to the launch's queries.
+    Not measured inside this run (PMC collection needs its own profiler passes)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    if world != 1 or not os.path.exists(path):
+        return None, None
+    try:
+        per_q = json.load(open(path)).get("hbm_bytes_per_query")
+        return (int(per_q * queries_per_launch) if per_q else None,
+                f"profiles/pmc_{config}.json (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, gfx950 "
+                f"corrections), bytes per query x {queries_per_launch}")
+    except (OSError, ValueError):
+        return None, None
+
+
+def r5(x):
+    return round(float(x), 5)
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--cpu-worker":
         return _cpu_worker(sys.argv[2:])
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + sorted(BATCH_CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS) + sorted(BATCH_CONFIGS),
+                    help="default: c24 on one GPU, c4 (split shard) on several")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--cpu-budget", type=float, default=20.0,
+                    help="seconds of single-core reference work (at least one full query)")
+    ap.add_argument("--cpu-cores", type=int, default=-1,
+                    help="processes of the all-cores reference leg (-1: this process's CPU "
+                         "share minus one; 0 or 1: skip)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="N=1: skip the configs[1] and 2^27 single-engine extra legs")
     ap.add_argument("--queue-only", action="store_true",
-                    help="profiling passes: only the warm-up and timed queues (every launch of "
-                         "the query kernel then answers the same number of queries)")
+                    help="profiling passes: only the warm-up and timed queues of the main "
+                         "workload (run with --warmup equal to --steps so every launch of the "
+                         "query kernel answers the same number of queries)")
     args = ap.parse_args()
 
     world, rank, local = dist_env()
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    if world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
     import torch
     import torch.distributed as dist
 
@@ -226,130 +409,64 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(local)
+    ctx = Ctx(world, rank, local)
 
     import erasurecodedpir_amd as pir
     from erasurecodedpir_amd.dist import broadcast_bytes, log2_exact
 
-    if args.config in BATCH_CONFIGS:
-        return run_batch(args, world, rank, local)
-    n_local, efs, p, nq, workload = CONFIGS[args.config]
+    config = args.config or ("c24" if world == 1 else "c4")
+    if config in BATCH_CONFIGS:
+        return run_batch(args, ctx, config)
+    n_cfg, efs, p, nq, strong, workload = CONFIGS[config]
     g = log2_exact(world)
-    n = n_local + g  # logical tree depth (weak scaling: 2^n_local records per GPU)
-    eng = pir.Engine(p, 1, n, efs, nq, device=local, log_num_partitions=g, partition_index=rank)
-    eng.fill_shard_random(0xC0FFEE)
-    if world > 1:
-        uid = broadcast_bytes(pir.comm_unique_id() if rank == 0 else None)
-        eng.attach_comm(uid, world, rank)
-    # K + W independent queries (distinct indices, fresh root seeds); every rank holds the same keys
-    # warm-up queue: at least W queries and as long as the timed queue, so that every launch of
-    # the queue kernel (warm-up, timed, profiled) answers K queries and rocprof's per-launch
-    # average is the timed launch's duration
-    nwarm = max(args.warmup, args.steps, 1)
-    nkeys = args.steps + nwarm
+    n = n_cfg if strong else n_cfg + g  # logical tree depth
+    W, K = args.warmup, args.steps
     seed = int.from_bytes(broadcast_bytes(os.urandom(8) if rank == 0 else None)
                           if world > 1 else os.urandom(8), "little")
     rng = np.random.default_rng(seed)
-    idxs = [int(i) for i in rng.choice(1 << n, nkeys, replace=False)]
-    idxs[0] = (1 << n) // 3 + 7
-    fcw = pir.final_cw(p, nq, 1)
-    keys = [pir.gen_keys(n, i, p, nq, fcw=fcw,
-                         seeds=rng.integers(0, 256, 16 * p, dtype=np.uint8).tobytes(), device=local)
-            for i in idxs]
-    kl, ab = eng.key_len, eng.answer_bytes
-    d_keys = eng.alloc_dev(kl * nkeys)
-    d_res = eng.alloc_dev(ab * nkeys)
-    eng.h2d(d_keys, b"".join(k[0] for k in keys))
-    W, K = nwarm, args.steps
-    d_kq, d_rq = d_keys + W * kl, d_res + W * ab  # the timed queue: keys W .. W+K-1
+    keyset, fcw = make_keys(pir, n, p, nq, W + K, rng, local)
 
-    def barrier_sync():
-        eng.sync()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-
-    def timed(fn):
-        barrier_sync()
-        t0 = time.perf_counter()
-        fn()
-        barrier_sync()
-        dt = time.perf_counter() - t0
-        if world > 1:
-            tt = torch.tensor([dt], dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            dt = float(tt.item())
-        return dt
-
-    # (1) the measurement: a queue of K independent queries (each its own DPF tree and its own
-    #     full pass over the shard), answered back to back in one launch after W warm-up queries
-    eng.reserve_queue(max(W, K))  # queue buffers sized at setup, as a server would
-    eng.answer_stream_dev(d_keys, W, d_res)
-    # HIP events on the engine stream bracket the query kernel inside the timed region (its
-    # duration feeds `roofline`; recording them costs microseconds, no synchronisation)
-    eng.set_profiling(1)
-    dt = timed(lambda: eng.answer_stream_dev(d_kq, K, d_rq))
-    phases_q = eng.last_timings()
-    eng.set_profiling(0)
-    ms = dt / K * 1e3
+    eng = pir.Engine(p, 1, n, efs, nq, device=local, log_num_partitions=g, partition_index=rank)
+    eng.fill_shard_random(SHARD_SEED)
+    if world > 1:
+        uid = broadcast_bytes(pir.comm_unique_id() if rank == 0 else None)
+        eng.attach_comm(uid, world, rank)
+    m = measure(ctx, eng, [ks[0] for _, ks in keyset], W, K, single=not args.queue_only)
+    ms = m["ms"]
+    shard_bytes = float(1 << n) * efs  # logical shard (all ranks)
+    value = shard_bytes / GIB / (ms / 1e3)
     if args.queue_only:
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": round(float(1 << n) * efs / GIB / (ms / 1e3), 3),
-                              "unit": "GiB/s", "ms_per_step": round(ms, 5), "steps": K,
-                              "warmup": W, "mode": "queue-only profiling pass"}), flush=True)
+            print(json.dumps({"metric": METRIC, "value": round(value, 3), "unit": "GiB/s",
+                              "ms_per_step": r5(ms), "steps": K, "warmup": W,
+                              "config": {"workload": workload},
+                              "mode": "queue-only profiling pass"}), flush=True)
         eng.close()
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
         return
-    queue_answers = eng.d2h(d_rq, ab * K).reshape(K, nq, efs)
-    # (3) one query at a time (answer_dev per step): single-query latency
-    for i in range(min(W, 5)):  # warm the one-query kernel (its own code object)
-        eng.answer_dev(d_keys + i * kl, d_res + i * ab)
-    dt1 = timed(lambda: [eng.answer_dev(d_kq + i * kl, d_rq + i * ab) for i in range(K)])
-    ms1 = dt1 / K * 1e3
-    single_answers = eng.d2h(d_rq, ab * K).reshape(K, nq, efs)
-    eng.set_profiling(max(K, 1))
-    for i in range(K):
-        eng.answer_dev(d_kq + i * kl, d_rq + i * ab)
-    phases1 = eng.last_timings()
-    eng.set_profiling(0)
-    alone = eng.profile_phases(d_keys, 10)
 
-    # PIR correctness at full size (every rank): party-1 ^ party-2 answers == finalCW * record
-    # (p=2) -- checked with the host API, which also gives the PCIe-inclusive rate.
-    k0 = keys[W][0]
+    timed = keyset[W:]
+    # PIR correctness at full size on every rank (the party-2 answers come from the same
+    # resident shard, answered as party 2)
+    pir_ok = pir_check(ctx, eng, timed[:4], fcw, m["answers"], n, g) if (p == 2 and nq == 1) else None
+    # host API (key H2D + answer D2H + sync): the PCIe-inclusive rate
+    k0 = timed[0][1][0]
     incl_steps = min(20, K)
     t1 = time.perf_counter()
     for _ in range(incl_steps):
         a1 = eng.answer(k0)
     incl_ms = (time.perf_counter() - t1) / incl_steps * 1e3
-    pir_ok = None
-    if p == 2 and nq == 1:
-        eng2 = pir.Engine(p, 2, n, efs, nq, device=local, log_num_partitions=g,
-                          partition_index=rank)
-        eng2.fill_shard_random(0xC0FFEE)
-        if world > 1:
-            uid2 = broadcast_bytes(pir.comm_unique_id() if rank == 0 else None)
-            eng2.attach_comm(uid2, world, rank)
-        a2 = eng2.answer(keys[W][1])
-        eng2.close()
-        idx = idxs[W]
-        owner = idx >> (n - g) if g else 0
-        rec = eng.shard_row(idx - owner * eng.num_rows) if rank == owner else None
-        if world > 1:
-            rec = broadcast_from(rec, owner, efs)
-        tab = _gf_table(int(fcw[0]))
-        pir_ok = bool(np.array_equal(a1[0] ^ a2[0], tab[rec]))
-    same = bool(np.array_equal(a1, single_answers[0]))
-    queue_same = bool(np.array_equal(queue_answers, single_answers))
+    same = bool(np.array_equal(a1, m["singles"][0]))
+    queue_same = bool(np.array_equal(m["answers"], m["singles"]))
 
-    shard_bytes = float(1 << n) * efs  # logical shard (all ranks)
-    value = shard_bytes / GIB / (ms / 1e3)
-    kern_ms = phases_q.get("scan", float("nan"))  # the k_query launch (all K queries)
+    ph = m["phases"]
     local_bytes = float(eng.num_rows) * efs
-    algo = local_bytes * K
-    achieved = algo / (kern_ms / 1e3) / 1e9 if kern_ms == kern_ms and kern_ms > 0 else None
-    path = {2.0: "k_query", 1.0: "k_fused", 0.0: "k_expand+k_scan"}.get(phases_q.get("fused"), "?")
+    kern_ms = ph.get("scan", float("nan"))  # the k_query launch (all K queries)
+    path = {2.0: "k_query", 1.0: "k_fused", 0.0: "k_expand+k_scan"}.get(ph.get("fused"), "?")
+    rl = roofline(kern_ms, local_bytes, K, config, world)
+    rl["kernel"] = rl["kernel"].replace("k_query", path)
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -357,121 +474,150 @@ def main():
         "n_gpus": world,
         "steps": K,
         "warmup": W,
-        "ms_per_step": round(ms, 5),
+        "ms_per_step": r5(ms),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
         "config": {
-            "workload": workload if world == 1 else f"split-shard (configs[3] layout): {world} x 2^{n_local} x {efs} B partitions of one 2^{n} x {efs} B logical shard, RCCL all-gather + XOR fold",
+            "workload": workload if world == 1 or strong else
+            f"split shard, weak scaling: {world} x 2^{n_cfg} x {efs} B partitions of one 2^{n} x {efs} B logical shard (RCCL all-gather + XOR fold)",
             "records": 1 << n, "record_bytes": efs, "parties": p, "num_rounds": nq,
             "records_per_gpu": int(eng.num_rows), "dpf_depth": n,
-            "parallelism": "split-shard" if world > 1 else "single",
+            "parallelism": f"split-shard x{world}" if world > 1 else "single",
             "step": "one PIR query: its own DPF key and tree, one full pass over the shard",
             "mode": "query queue: the K timed queries (distinct keys) are answered back to back "
                     "in one launch, the tree of query k+1 built while query k streams",
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": f"{path} (DPF tree + GF(2^8) shard scan, {K} queries per launch)",
-            "achieved": round(achieved, 1) if achieved else None,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": _pmc_traffic(args.config, world, K),
-            "algorithmic_bytes_per_launch": int(algo),
-            "algorithmic_bytes_per_query": int(local_bytes),
-            "kernel_ms_per_launch": round(kern_ms, 5),
-        },
+        "roofline": rl,
         "single_query": {
-            "ms_per_query": round(ms1, 5),
-            "value": round(shard_bytes / GIB / (ms1 / 1e3), 3),
+            "ms_per_query": r5(m["ms1"]),
+            "value": round(shard_bytes / GIB / (m["ms1"] / 1e3), 3),
             "unit": "GiB/s",
             "note": "answer_dev per step (one launch per query, nothing queued behind it)",
-            "phases_ms": {k: round(v, 5) for k, v in phases1.items() if k != "chunks"},
+            "phases_ms": {k: r5(v) for k, v in m["phases1"].items() if k != "chunks"},
         },
-        "phases_alone_ms": {k: round(v, 5) for k, v in alone.items()},
         "inclusive_h2d_key_d2h_answer": {"ms_per_query": round(incl_ms, 4),
                                          "value": round(shard_bytes / GIB / (incl_ms / 1e3), 3),
                                          "unit": "GiB/s"},
         "parity": {"pir_record_recovered": pir_ok, "host_api_equals_device_api": same,
                    "queue_equals_one_at_a_time": queue_same},
     }
+    if world > 1:  # per-rank kernel and exchange times of the timed queue
+        mine = {"rank": rank, "k_query_ms": r5(kern_ms), "reduce_ms": r5(ph.get("reduce", 0)),
+                "allgather_xor_fold_ms": r5(ph.get("comm_fold", 0)),
+                "queue_total_ms": r5(ph.get("total", 0))}
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+        out["per_rank"] = allr
+    cpu_path = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        shard_rows = eng.get_shard()
-        out["cpu_baseline"] = cpu_baseline(k0, shard_rows, n, efs, p, nq, single_answers[0],
-                                           args.cpu_budget)
-        out["parity"]["gpu_equals_cpu_reference"] = out["cpu_baseline"]["bit_exact_vs_gpu"]
-        del shard_rows
+        cpu_path = shard_file_path(int(local_bytes))
+        dump_shard(eng, cpu_path)
+    cpu_key, cpu_want = k0, m["singles"][0]
+    eng.close()
+
+    if strong and world > 1:
+        # the same K queries answered by ONE GPU holding the whole logical shard (rank 0's GPU,
+        # after its partition engine is freed): the 1-GPU point of the strong-scaling curve
+        if rank == 0:
+            e1 = pir.Engine(p, 1, n, efs, nq, device=local)
+            e1.fill_shard_random(SHARD_SEED)
+            solo = Ctx(1, 0, local)
+            m1 = measure(solo, e1, [ks[0] for _, ks in keyset], min(W, 2), K, single=False)
+            e1.close()
+            v1 = shard_bytes / GIB / (m1["ms"] / 1e3)
+            out["n1_reference"] = {
+                "ms_per_query": r5(m1["ms"]), "value": round(v1, 3), "unit": "GiB/s",
+                "k_query_ms": r5(m1["phases"].get("scan", 0)),
+                "answers_equal_split_shard": bool(np.array_equal(m1["answers"], m["answers"])),
+                "note": "the same K queries answered by one engine holding the whole 2^27 x 1 KiB "
+                        "shard (128 GiB) on rank 0's GPU"}
+            out["speedup_vs_1gpu"] = round(value / v1, 3)
+        dist.barrier()
+
+    if rank == 0 and world == 1 and not args.no_extras:
+        out["configs1_c2"] = extra_leg(ctx, pir, "c2", W, K, rng)
+        if config != "c4":
+            out["c4_single_engine"] = extra_leg(ctx, pir, "c4", min(W, 2), min(K, 8), rng,
+                                                single=False)
+    if cpu_path:
+        try:
+            cores = _host_cores() if args.cpu_cores < 0 else args.cpu_cores
+            out["cpu_baseline"] = cpu_baseline(cpu_path, n, efs, p, nq, cpu_key, cpu_want,
+                                               args.cpu_budget, cores)
+            out["parity"]["gpu_equals_cpu_reference"] = out["cpu_baseline"]["bit_exact_vs_gpu"]
+        finally:
+            os.unlink(cpu_path)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def run_batch(args, world, rank, local):
+def extra_leg(ctx, pir, config, W, K, rng, single=True):
+    """Another workload on this GPU (N = 1): queue and single-query rates."""
+    n, efs, p, nq, _, workload = CONFIGS[config]
+    keyset, fcw = make_keys(pir, n, p, nq, W + K, rng, ctx.local)
+    eng = pir.Engine(p, 1, n, efs, nq, device=ctx.local)
+    eng.fill_shard_random(SHARD_SEED)
+    m = measure(ctx, eng, [ks[0] for _, ks in keyset], W, K, single=single)
+    ok = pir_check(ctx, eng, keyset[W:W + 2], fcw, m["answers"], n, 0) if (p == 2 and nq == 1) else None
+    eng.close()
+    gib = float(1 << n) * efs / GIB
+    kern = m["phases"].get("scan", float("nan"))
+    res = {"workload": workload, "steps": K, "warmup": W, "ms_per_query": r5(m["ms"]),
+           "value": round(gib / (m["ms"] / 1e3), 3), "unit": "GiB/s",
+           "k_query_ms_per_launch": r5(kern),
+           "roofline_frac": round(gib * GIB * K / (kern / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if kern > 0 else None,
+           "pir_record_recovered": ok}
+    if single:
+        res["single_query"] = {"ms_per_query": r5(m["ms1"]),
+                               "value": round(gib / (m["ms1"] / 1e3), 3), "unit": "GiB/s",
+                               "note": "batch = 1: one launch per query"}
+        res["queue_equals_one_at_a_time"] = bool(np.array_equal(m["answers"], m["singles"]))
+    return res
+
+
+def run_batch(args, ctx, config):
     """A step = `batch` keys answered against the device-resident shard (answer_batch_dev: one
     shard pass per group of keys, one DPF tree per key).  value = effective GiB/s = keys x
     logical shard bytes / time (every key's answer covers the whole shard)."""
-    import torch
-    import torch.distributed as dist
     import erasurecodedpir_amd as pir
     from erasurecodedpir_amd.dist import broadcast_bytes, log2_exact
 
-    n_local, efs, p, nq, nk, workload = BATCH_CONFIGS[args.config]
+    world, rank, local = ctx.world, ctx.rank, ctx.local
+    n_local, efs, p, nq, nk, workload = BATCH_CONFIGS[config]
     g = log2_exact(world)
     n = n_local + g
     eng = pir.Engine(p, 1, n, efs, nq, device=local, log_num_partitions=g, partition_index=rank)
-    eng.fill_shard_random(0xC0FFEE)
+    eng.fill_shard_random(SHARD_SEED)
     if world > 1:
         uid = broadcast_bytes(pir.comm_unique_id() if rank == 0 else None)
         eng.attach_comm(uid, world, rank)
     rng = np.random.default_rng(int.from_bytes(
         broadcast_bytes(os.urandom(8) if rank == 0 else None) if world > 1 else os.urandom(8), "little"))
-    idxs = [int(i) for i in rng.choice(1 << n, nk, replace=False)]
-    fcw = pir.final_cw(p, nq, 1)
-    keys = [pir.gen_keys(n, i, p, nq, fcw=fcw, seeds=rng.integers(0, 256, 16 * p, dtype=np.uint8).tobytes(),
-                         device=local) for i in idxs]
+    keyset, fcw = make_keys(pir, n, p, nq, nk, rng, local)
     d_keys = eng.alloc_dev(eng.key_len * nk)
     d_res = eng.alloc_dev(eng.answer_bytes * nk)
-    eng.h2d(d_keys, b"".join(k[0] for k in keys))
-
-    def barrier_sync():
-        eng.sync()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-
+    eng.h2d(d_keys, b"".join(ks[0] for _, ks in keyset))
     for _ in range(args.warmup):
         eng.answer_batch_dev(d_keys, nk, d_res)
-    barrier_sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.answer_batch_dev(d_keys, nk, d_res)
-    barrier_sync()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    eng.set_profiling(max(1, args.steps))
+    dt = ctx.timed(eng, lambda: [eng.answer_batch_dev(d_keys, nk, d_res) for _ in range(args.steps)])
+    eng.set_profiling(0)
     ms = dt / args.steps * 1e3
-    # one key alone (fused single-query path) and its tree / scan phases, for reference
     alone = eng.profile_phases(d_keys, 5)
     got = eng.d2h(d_res, eng.answer_bytes * nk).reshape(nk, nq, efs)
     # correctness at full size: party-1 batch ^ party-2 batch == finalCW * record, every key
-    eng2 = pir.Engine(p, 2, n, efs, nq, device=local, log_num_partitions=g, partition_index=rank)
-    eng2.fill_shard_random(0xC0FFEE)
-    if world > 1:
-        uid2 = broadcast_bytes(pir.comm_unique_id() if rank == 0 else None)
-        eng2.attach_comm(uid2, world, rank)
-    got2 = eng2.answer_batch([k[1] for k in keys])
-    eng2.close()
+    eng.set_party(2)
+    got2 = eng.answer_batch([ks[1] for _, ks in keyset])
+    eng.set_party(1)
     tab = _gf_table(int(fcw[0]))
     ok = True
-    for q, i in enumerate(idxs):
+    for q, (i, _) in enumerate(keyset):
         owner = i >> (n - g) if g else 0
         rec = eng.shard_row(i - owner * eng.num_rows) if rank == owner else None
         if world > 1:
@@ -493,15 +639,15 @@ def run_batch(args, world, rank, local):
         "ms_per_key": round(ms / nk, 5),
         "keys_per_s": round(nk / (ms / 1e3), 1),
         "shard_passes_per_step": -(-nk // eng.batch_group),
-        "single_key_phases_alone_ms": {k: round(v, 5) for k, v in alone.items()},
+        "single_key_phases_alone_ms": {k: r5(v) for k, v in alone.items()},
         "parity": {"pir_record_recovered_all_keys": ok},
     }
+    eng.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
     if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+        ctx.dist.barrier()
+        ctx.dist.destroy_process_group()
 
 
 def broadcast_from(arr, src, nbytes):
@@ -510,32 +656,6 @@ def broadcast_from(arr, src, nbytes):
     t = torch.from_numpy(arr.copy()) if arr is not None else torch.zeros(nbytes, dtype=torch.uint8)
     dist.broadcast(t, src=src)
     return t.numpy()
-
-
-def _gf_table(c):
-    t = np.zeros(256, np.uint8)
-    for x in range(256):
-        a, b, r = c, x, 0
-        while b:
-            if b & 1:
-                r ^= a
-            a = ((a << 1) ^ (0x11D if a & 0x80 else 0)) & 0xFF
-            b >>= 1
-        t[x] = r
-    return t
-
-
-def _pmc_traffic(config, world, queries_per_launch):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc passes
-    (profiles/pmc_<config>.json: bytes per query, measured), scaled to the launch's queries."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
-    if world != 1 or not os.path.exists(path):
-        return None
-    try:
-        per_q = json.load(open(path)).get("hbm_bytes_per_query")
-        return int(per_q * queries_per_launch) if per_q else None
-    except (OSError, ValueError):
-        return None
 
 
 if __name__ == "__main__":

@@ -84,6 +84,8 @@ PROTOTYPES = {
     "pir_engine_stream": (_P, [_P]),
     "pir_engine_sync": (_I, [_P]),
     "pir_engine_alloc_dev": (_I, [_P, _SZ, ctypes.POINTER(_P)]),
+    "pir_engine_free_dev": (_I, [_P, _P]),
+    "pir_engine_set_party_index": (_I, [_P, _I]),
     "pir_engine_memcpy_h2d": (_I, [_P, _P, _P, _SZ]),
     "pir_engine_memcpy_d2h": (_I, [_P, _P, _P, _SZ]),
     "pir_engine_set_profiling": (_I, [_P, _I]),

@@ -128,6 +128,11 @@ struct pir_engine {
   std::vector<ProfSlot> prof;
   int prof_next = 0, prof_count = 0;
   hipEvent_t* ev = nullptr;  // the current answer's slot (nullptr: profiling off)
+  // the engine's work buffers (slabs, tree nodes, share buffers, staged keys) are shared by
+  // every answer: an answer enqueued on a stream other than the previous answer's waits for
+  // that answer's last use of them (ev_ws, recorded after every answer)
+  hipEvent_t ev_ws = nullptr;
+  hipStream_t ws_stream = nullptr;
   // RCCL
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -401,6 +406,19 @@ int answer_batch_core(pir_engine* e, const uint8_t* d_raw, int nk, int log_parts
 
 int check_key_ptr(const void* p) { return p ? PIR_OK : fail(PIR_EINVAL, "null key"); }
 
+// before an answer on stream s: order it after the previous answer's use of the workspace
+int ws_acquire(pir_engine* e, hipStream_t s) {
+  if (e->ws_stream && e->ws_stream != s) HIP_TRY(hipStreamWaitEvent(s, e->ev_ws, 0));
+  return PIR_OK;
+}
+// after it: the next answer, on whatever stream, waits for this one
+int ws_release(pir_engine* e, hipStream_t s, int rc) {
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(e->ev_ws, s));
+  e->ws_stream = s;
+  return PIR_OK;
+}
+
 const char* const kPhaseNames[] = {"key_prep", "tree_frontier", "tree_leaves", "scan",
                                    "reduce", "comm_fold", "total", "chunks", "fused"};
 constexpr int kNumPhases = 9;
@@ -600,7 +618,8 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
       return cleanup(fail(PIR_EHIP, "hipEventCreate failed"));
   if (hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_ws, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail(PIR_EHIP, "hipEventCreate failed"));
   for (int i = 0; i < 2; ++i)
     if (hipEventCreateWithFlags(&e->ev_cb_ready[i], hipEventDisableTiming) != hipSuccess ||
@@ -673,6 +692,7 @@ void pir_engine_destroy(pir_engine_t* e) {
   }
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+  if (e->ev_ws) (void)hipEventDestroy(e->ev_ws);
   if (e->aux) (void)hipStreamDestroy(e->aux);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -761,7 +781,8 @@ int pir_engine_answer_dev(pir_engine_t* e, const uint8_t* d_key, uint8_t* d_resu
   std::lock_guard<std::mutex> lk(e->mu);
   HIP_TRY(hipSetDevice(e->cfg.device));
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  return answer_dev_locked(e, d_key, d_result, s);
+  if (int rc = ws_acquire(e, s)) return rc;
+  return ws_release(e, s, answer_dev_locked(e, d_key, d_result, s));
 }
 
 int pir_engine_answer_batch_dev(pir_engine_t* e, const uint8_t* d_keys, int num_keys,
@@ -771,7 +792,8 @@ int pir_engine_answer_batch_dev(pir_engine_t* e, const uint8_t* d_keys, int num_
   std::lock_guard<std::mutex> lk(e->mu);
   HIP_TRY(hipSetDevice(e->cfg.device));
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  return answer_batch_locked(e, d_keys, num_keys, d_result, s);
+  if (int rc = ws_acquire(e, s)) return rc;
+  return ws_release(e, s, answer_batch_locked(e, d_keys, num_keys, d_result, s));
 }
 
 int pir_engine_answer_batch(pir_engine_t* e, const uint8_t* keys, int num_keys,
@@ -789,10 +811,10 @@ int pir_engine_answer_batch(pir_engine_t* e, const uint8_t* keys, int num_keys,
     (void)hipFree(d_k);
     return fail(PIR_ENOMEM, "batch result buffer %zu bytes", rb);
   }
-  int rc = PIR_OK;
-  if (hipMemcpyAsync(d_k, keys, kb, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+  int rc = ws_acquire(e, e->stream);
+  if (!rc && hipMemcpyAsync(d_k, keys, kb, hipMemcpyHostToDevice, e->stream) != hipSuccess)
     rc = fail(PIR_EHIP, "key upload");
-  if (!rc) rc = answer_batch_locked(e, d_k, num_keys, d_r, e->stream);
+  if (!rc) rc = ws_release(e, e->stream, answer_batch_locked(e, d_k, num_keys, d_r, e->stream));
   if (!rc && (hipMemcpyAsync(results, d_r, rb, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
               hipStreamSynchronize(e->stream) != hipSuccess))
     rc = fail(PIR_EHIP, "batch answer: %s", hipGetErrorString(hipGetLastError()));
@@ -809,7 +831,8 @@ int pir_engine_answer_stream_dev(pir_engine_t* e, const uint8_t* d_keys, int num
   std::lock_guard<std::mutex> lk(e->mu);
   HIP_TRY(hipSetDevice(e->cfg.device));
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  return answer_stream_locked(e, d_keys, num_keys, d_result, s);
+  if (int rc = ws_acquire(e, s)) return rc;
+  return ws_release(e, s, answer_stream_locked(e, d_keys, num_keys, d_result, s));
 }
 
 int pir_engine_reserve_queue(pir_engine_t* e, int num_keys) {
@@ -845,9 +868,10 @@ int pir_engine_answer(pir_engine_t* e, const uint8_t* key, uint8_t* result) {
   std::lock_guard<std::mutex> lk(e->mu);
   HIP_TRY(hipSetDevice(e->cfg.device));
   const size_t out_bytes = (size_t)e->cfg.num_rounds * e->cfg.record_bytes;
+  if (int rc = ws_acquire(e, e->stream)) return rc;
   memcpy(e->h_key, key, e->key_len);
   HIP_TRY(hipMemcpyAsync(e->d_key_raw, e->h_key, e->key_len, hipMemcpyHostToDevice, e->stream));
-  int rc = answer_dev_locked(e, e->d_key_raw, e->d_result, e->stream);
+  int rc = ws_release(e, e->stream, answer_dev_locked(e, e->d_key_raw, e->d_result, e->stream));
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(e->h_res, e->d_result, out_bytes, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -871,12 +895,14 @@ int pir_engine_answer_slice(pir_engine_t* e, const uint8_t* key, int thread_num,
   const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
   // NB: the reference's Thread variant computes the honest answer even when isByzantine is
   // set (both branches of server.cpp:526-541 are identical); mirrored here.
+  if (int rc = ws_acquire(e, e->stream)) return rc;
   memcpy(e->h_key, key, e->key_len);
   HIP_TRY(hipMemcpyAsync(e->d_key_raw, e->h_key, e->key_len, hipMemcpyHostToDevice, e->stream));
   const uint64_t prefix = ((uint64_t)c.partition_index << lt) | (uint64_t)thread_num;
   const uint64_t row0 = (uint64_t)thread_num * (e->rows >> lt);
-  int rc = answer_core(e, e->d_key_raw, c.log_num_partitions + lt, prefix, row0, e->d_result,
-                       e->stream);
+  int rc = ws_release(e, e->stream,
+                      answer_core(e, e->d_key_raw, c.log_num_partitions + lt, prefix, row0,
+                                  e->d_result, e->stream));
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(e->h_res, e->d_result, out_bytes, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -890,6 +916,7 @@ int pir_engine_eval_all(pir_engine_t* e, const uint8_t* key, uint8_t* out) {
   std::lock_guard<std::mutex> lk(e->mu);
   const auto& c = e->cfg;
   HIP_TRY(hipSetDevice(c.device));
+  if (int rc = ws_acquire(e, e->stream)) return rc;
   memcpy(e->h_key, key, e->key_len);
   HIP_TRY(hipMemcpyAsync(e->d_key_raw, e->h_key, e->key_len, hipMemcpyHostToDevice, e->stream));
   const pir::TreePlan pl =
@@ -899,6 +926,7 @@ int pir_engine_eval_all(pir_engine_t* e, const uint8_t* key, uint8_t* out) {
   std::vector<uint8_t> ct((size_t)e->rows * e->nrp);
   HIP_TRY(hipMemcpyAsync(ct.data(), e->d_c, ct.size(), hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  e->ws_stream = nullptr;  // synchronised: nothing left to order after
   for (uint64_t i = 0; i < e->rows; ++i)
     for (int a = 0; a < c.num_rounds; ++a) out[(size_t)a * e->rows + i] = ct[i * e->nrp + a];
   return PIR_OK;
@@ -922,6 +950,30 @@ int pir_engine_alloc_dev(pir_engine_t* e, size_t bytes, void** d_ptr) {
   e->user.push_back({p, bytes});
   *d_ptr = p;
   return PIR_OK;
+}
+
+int pir_engine_free_dev(pir_engine_t* e, void* d_ptr) {
+  if (!e) return fail(PIR_EINVAL, "null engine");
+  if (!d_ptr) return PIR_OK;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  for (size_t i = 0; i < e->user.size(); ++i)
+    if (e->user[i].p == d_ptr) {
+      // answers still queued on any stream may read it: hipFree waits for the device
+      HIP_TRY(hipFree(d_ptr));
+      e->user.erase(e->user.begin() + (long)i);
+      return PIR_OK;
+    }
+  return fail(PIR_EINVAL, "%p was not allocated by pir_engine_alloc_dev", d_ptr);
+}
+
+int pir_engine_set_party_index(pir_engine_t* e, int party_index) {
+  if (!e) return fail(PIR_EINVAL, "null engine");
+  if (party_index < 1 || party_index > e->cfg.num_parties)
+    return fail(PIR_EINVAL, "party_index %d outside [1,%d]", party_index, e->cfg.num_parties);
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->cfg.party_index = party_index;  // read at enqueue time (a kernel argument), not by kernels
+  return PIR_OK;                     // already queued
 }
 
 int pir_engine_memcpy_h2d(pir_engine_t* e, void* d_dst, const void* h_src, size_t bytes) {
@@ -967,6 +1019,8 @@ int pir_engine_profile_phases(pir_engine_t* e, const uint8_t* d_key, int iters, 
   const auto& c = e->cfg;
   HIP_TRY(hipSetDevice(c.device));
   hipStream_t s = e->stream;
+  if (int rc = ws_acquire(e, s)) return rc;
+  e->ws_stream = nullptr;  // synchronised below
   const pir::TreePlan pl =
       pir::make_plan(c.log_num_records, c.log_num_partitions, (uint64_t)c.partition_index);
   const pir::ScanShape sh = pir::make_scan_shape(pl.nleaves, e->pitch, c.num_rounds, e->num_cus);
@@ -1010,6 +1064,8 @@ int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, int num_keys, 
                                                  c.num_parties, c.num_rounds, e->pitch, e->num_cus,
                                                  num_keys);
   if (!qp.tile) return fail(PIR_EINVAL, "shape does not use the single-launch query kernel");
+  if (int rc = ws_acquire(e, e->stream)) return rc;
+  e->ws_stream = nullptr;  // synchronised below
   const pir::ScanShape& sh = qp.shape;
   int rc = ensure_slabs(e, (size_t)num_keys * pir::query_slab_bytes(qp));
   if (!rc) rc = ensure_buf(&e->d_qscratch, &e->qscratch_cap, pir::query_scratch_bytes(qp));

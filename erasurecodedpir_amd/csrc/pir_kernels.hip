@@ -1523,11 +1523,12 @@ __global__ __launch_bounds__(kReduceThreads) void k_reduce(const uint32_t* __res
 
 __global__ void k_xor_fold(const uint8_t* __restrict__ in, int nranks, size_t len,
                            uint8_t* __restrict__ out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= len) return;
-  uint8_t acc = 0;
-  for (int r = 0; r < nranks; ++r) acc ^= in[(size_t)r * len + i];
-  out[i] = acc;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < len;
+       i += (size_t)gridDim.x * blockDim.x) {
+    uint8_t acc = 0;
+    for (int r = 0; r < nranks; ++r) acc ^= in[(size_t)r * len + i];
+    out[i] = acc;
+  }
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
@@ -1538,31 +1539,33 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
 }
 
 __global__ void k_fill_random(uint8_t* __restrict__ d, size_t bytes, uint64_t seed) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < bytes) d[i] = (uint8_t)splitmix64(seed ^ (i * 0xD1B54A32D192ED03ull));
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < bytes;
+       i += (size_t)gridDim.x * blockDim.x)
+    d[i] = (uint8_t)splitmix64(seed ^ (i * 0xD1B54A32D192ED03ull));
 }
 
 // byte b of global row i = byte (b & 7) of splitmix64(seed ^ (i << 20 | b >> 3)); padding 0
 __global__ void k_fill_shard(uint8_t* __restrict__ shard, uint64_t rows, uint32_t pitch,
                              uint32_t efs, uint64_t row0, uint64_t seed) {
   const uint32_t cpr = pitch / 16;
-  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= rows * cpr) return;
-  const uint64_t r = idx / cpr;
-  const uint32_t ch = (uint32_t)(idx - r * cpr);
-  const uint64_t gr = row0 + r;
-  uint32_t w[4];
-  for (int h = 0; h < 2; ++h) {
-    const uint32_t b = ch * 16 + h * 8;
-    const uint64_t z = splitmix64(seed ^ ((gr << 20) | (b >> 3)));
-    w[2 * h] = (uint32_t)z;
-    w[2 * h + 1] = (uint32_t)(z >> 32);
+  for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < rows * cpr;
+       idx += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = idx / cpr;
+    const uint32_t ch = (uint32_t)(idx - r * cpr);
+    const uint64_t gr = row0 + r;
+    uint32_t w[4];
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t b = ch * 16 + h * 8;
+      const uint64_t z = splitmix64(seed ^ ((gr << 20) | (b >> 3)));
+      w[2 * h] = (uint32_t)z;
+      w[2 * h + 1] = (uint32_t)(z >> 32);
+    }
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t b = ch * 16 + k;
+      if (b >= efs) w[k >> 2] &= ~(0xffu << (8 * (k & 3)));
+    }
+    *reinterpret_cast<uint4*>(shard + r * pitch + ch * 16) = make_uint4(w[0], w[1], w[2], w[3]);
   }
-  for (int k = 0; k < 16; ++k) {
-    const uint32_t b = ch * 16 + k;
-    if (b >= efs) w[k >> 2] &= ~(0xffu << (8 * (k & 3)));
-  }
-  *reinterpret_cast<uint4*>(shard + r * pitch + ch * 16) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1600,40 +1603,41 @@ __global__ void k_encode_across(const uint8_t* __restrict__ files, uint64_t fpit
                                 uint8_t* __restrict__ shard, uint64_t rows, uint64_t row0,
                                 uint32_t pitch, uint32_t efs) {
   const uint32_t cpr = pitch / 16;
-  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= rows * cpr) return;
-  const uint64_t r = idx / cpr;
-  const uint32_t ch = (uint32_t)(idx - r * cpr);
-  const uint64_t gr = row0 + r;
-  uint4 acc = make_uint4(0, 0, 0, 0);
-  for (int j = 0; j < k; ++j) {
-    const uint64_t src = encdb * (uint64_t)j + gr;
-    if (src >= nfiles) continue;
-    uint4 x;
-    if (files && (fpitch & 15u) == 0 && ch * 16u + 16u <= efs) {  // aligned whole chunk
-      x = *reinterpret_cast<const uint4*>(files + src * fpitch + ch * 16u);
-    } else if (files) {
-      uint32_t w[4];
-      const uint8_t* f = files + src * fpitch + ch * 16u;
-      for (int t = 0; t < 4; ++t) {
-        uint32_t v = 0;
-        for (int u = 0; u < 4; ++u) {
-          const uint32_t bi = ch * 16u + 4u * t + u;
-          if (bi < efs) v |= (uint32_t)f[4 * t + u] << (8 * u);
+  for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < rows * cpr;
+       idx += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = idx / cpr;
+    const uint32_t ch = (uint32_t)(idx - r * cpr);
+    const uint64_t gr = row0 + r;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < k; ++j) {
+      const uint64_t src = encdb * (uint64_t)j + gr;
+      if (src >= nfiles) continue;
+      uint4 x;
+      if (files && (fpitch & 15u) == 0 && ch * 16u + 16u <= efs) {  // aligned whole chunk
+        x = *reinterpret_cast<const uint4*>(files + src * fpitch + ch * 16u);
+      } else if (files) {
+        uint32_t w[4];
+        const uint8_t* f = files + src * fpitch + ch * 16u;
+        for (int t = 0; t < 4; ++t) {
+          uint32_t v = 0;
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t bi = ch * 16u + 4u * t + u;
+            if (bi < efs) v |= (uint32_t)f[4 * t + u] << (8 * u);
+          }
+          w[t] = v;
         }
-        w[t] = v;
+        x = make_uint4(w[0], w[1], w[2], w[3]);
+      } else {
+        x = make_uint4(synth_word(src, ch * 16u), synth_word(src, ch * 16u + 4),
+                       synth_word(src, ch * 16u + 8), synth_word(src, ch * 16u + 12));
       }
-      x = make_uint4(w[0], w[1], w[2], w[3]);
-    } else {
-      x = make_uint4(synth_word(src, ch * 16u), synth_word(src, ch * 16u + 4),
-                     synth_word(src, ch * 16u + 8), synth_word(src, ch * 16u + 12));
+      acc = xor4(acc, gf_mul_const4(x, co.c[j]));
     }
-    acc = xor4(acc, gf_mul_const4(x, co.c[j]));
+    uint32_t w[4] = {acc.x, acc.y, acc.z, acc.w};
+    for (int t = 0; t < 16; ++t)
+      if (ch * 16u + t >= efs) w[t >> 2] &= ~(0xffu << (8 * (t & 3)));  // zero pad bytes
+    *reinterpret_cast<uint4*>(shard + r * pitch + ch * 16u) = make_uint4(w[0], w[1], w[2], w[3]);
   }
-  uint32_t w[4] = {acc.x, acc.y, acc.z, acc.w};
-  for (int t = 0; t < 16; ++t)
-    if (ch * 16u + t >= efs) w[t >> 2] &= ~(0xffu << (8 * (t & 3)));  // zero pad bytes
-  *reinterpret_cast<uint4*>(shard + r * pitch + ch * 16u) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2040,15 +2044,21 @@ hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t e
   return hipGetLastError();
 }
 
+// grid-stride kernels of 256 threads: enough workgroups to fill the chip many times over, and
+// never past the 2^32 threads a launch may have (a 2^27-row shard has 2^33 16-byte chunks)
+static unsigned grid_1d(uint64_t items) {
+  return (unsigned)std::min<uint64_t>((items + 255) / 256, 1u << 16);
+}
+
 hipError_t launch_xor_fold(const uint8_t* d_in, int nranks, size_t len, uint8_t* d_out,
                            hipStream_t s) {
-  hipLaunchKernelGGL(k_xor_fold, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, d_in,
+  hipLaunchKernelGGL(k_xor_fold, dim3(grid_1d(len)), dim3(256), 0, s, d_in,
                      nranks, len, d_out);
   return hipGetLastError();
 }
 
 hipError_t launch_fill_random(uint8_t* d, size_t bytes, uint64_t seed, hipStream_t s) {
-  hipLaunchKernelGGL(k_fill_random, dim3((unsigned)((bytes + 255) / 256)), dim3(256), 0, s, d,
+  hipLaunchKernelGGL(k_fill_random, dim3(grid_1d(bytes)), dim3(256), 0, s, d,
                      bytes, seed);
   return hipGetLastError();
 }
@@ -2073,7 +2083,7 @@ hipError_t launch_encode_across(const uint8_t* d_files, uint64_t file_pitch, uin
   }
   const uint64_t encdb = (nfiles + k - 1) / k;
   const uint64_t total = rows * (pitch / 16);
-  hipLaunchKernelGGL(k_encode_across, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+  hipLaunchKernelGGL(k_encode_across, dim3(grid_1d(total)), dim3(256), 0, s,
                      d_files, file_pitch, nfiles, encdb, k, co, d_shard, rows, row0, pitch, efs);
   return hipGetLastError();
 }
@@ -2081,7 +2091,7 @@ hipError_t launch_encode_across(const uint8_t* d_files, uint64_t file_pitch, uin
 hipError_t launch_fill_shard(uint8_t* d_shard, uint64_t rows, uint32_t pitch, uint32_t efs,
                              uint64_t global_row0, uint64_t seed, hipStream_t s) {
   const uint64_t total = rows * (pitch / 16);
-  hipLaunchKernelGGL(k_fill_shard, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+  hipLaunchKernelGGL(k_fill_shard, dim3(grid_1d(total)), dim3(256), 0, s,
                      d_shard, rows, pitch, efs, global_row0, seed);
   return hipGetLastError();
 }

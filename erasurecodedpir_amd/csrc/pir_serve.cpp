@@ -236,7 +236,7 @@ struct Server {
   int party = 1, device = 0, byzantine = 0;
   std::mutex mu;
   pir_engine_t* eng = nullptr;
-  int nq = 0, efs = 0;
+  int nq = 0, efs = 0, key_len = 0;  // of the current engine (the params globals may move on)
 };
 Server g;
 
@@ -250,11 +250,14 @@ std::string setup(const MVal& req) {  // server.go:295-331
   if (t != 1 || b != 0) return "tree mode needs T = 1 and B = 0";
   if (log_files < 0 || log_files > 40 || fsz < 1 || k < 1 || k > 16 || r < 0 || rho < 1)
     return "bad setup parameters";
-  setSystemParams(log_files, fsz, t, k, r, b, rho, mac, mode);
-  if (g.party > NUM_PARTIES) return "this server's party index exceeds NUM_PARTIES";
+  // the process-global sizing (params.cpp) and the engine change together, under g.mu: a
+  // concurrent TREE_SEARCH sees either the old engine and its sizes or the new ones
   std::lock_guard<std::mutex> lk(g.mu);
   if (g.eng) pir_engine_destroy(g.eng);
   g.eng = nullptr;
+  g.key_len = 0;
+  setSystemParams(log_files, fsz, t, k, r, b, rho, mac, mode);
+  if (g.party > NUM_PARTIES) return "this server's party index exceeds NUM_PARTIES";
   pir_engine_config c{};
   c.device = g.device;
   c.num_parties = NUM_PARTIES;
@@ -269,6 +272,7 @@ std::string setup(const MVal& req) {  // server.go:295-331
     return std::string("encode: ") + pir_engine_last_error();
   g.nq = NUM_ROUNDS;
   g.efs = ENCODED_FILE_SIZE_BYTES;
+  g.key_len = pir_engine_key_len(c.num_parties, c.log_num_records, c.num_rounds);
   return "";
 }
 
@@ -292,14 +296,17 @@ void handle(SSL* ssl) {
     } else if (type == TREE_SEARCH_REQUEST) {  // tree.go:17-101
       const MVal* key = req.get("Key");
       std::vector<uint8_t> out;
+      int nq = 0, efs = 0;  // this answer's shape, read under the lock with the engine
       {
         std::lock_guard<std::mutex> lk(g.mu);
+        nq = g.nq;
+        efs = g.efs;
         if (!g.eng) err = "query before setup";
         else if (!key || (key->kind != MVal::BIN && key->kind != MVal::STR) ||
-                 (int)key->s.size() != pir_engine_key_len(NUM_PARTIES, LOG_NUM_ENCODED_FILES, g.nq))
+                 (int)key->s.size() != g.key_len)  // the engine's own key length
           err = "bad key";
         else {
-          out.resize((size_t)g.nq * g.efs);
+          out.resize((size_t)nq * efs);
           if (pir_engine_answer(g.eng, (const uint8_t*)key->s.data(), out.data()) != PIR_OK)
             err = std::string("answer: ") + pir_engine_last_error();
         }
@@ -308,8 +315,8 @@ void handle(SSL* ssl) {
       w.map(5);
       w.str("Results");
       if (err.empty()) {
-        w.array((size_t)g.nq);
-        for (int a = 0; a < g.nq; ++a) w.bin(out.data() + (size_t)a * g.efs, (size_t)g.efs);
+        w.array((size_t)nq);
+        for (int a = 0; a < nq; ++a) w.bin(out.data() + (size_t)a * efs, (size_t)efs);
       } else {
         w.array(0);
       }

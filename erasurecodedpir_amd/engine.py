@@ -87,9 +87,14 @@ class Engine:
             f = np.ascontiguousarray(np.asarray(files, np.uint8).reshape(num_files, -1))
             pitch = f.shape[1]
             d_f = self.alloc_dev(f.size)
-            self.h2d(d_f, f.reshape(-1))
-        check(self._lib.pir_engine_encode_across_dev(self._h, d_f, pitch, num_files, k),
-              "encode_across")
+        try:
+            if d_f is not None:
+                self.h2d(d_f, f.reshape(-1))
+            check(self._lib.pir_engine_encode_across_dev(self._h, d_f, pitch, num_files, k),
+                  "encode_across")
+        finally:
+            if d_f is not None:
+                self.free_dev(d_f)
 
     def shard_row(self, i):
         out = np.empty(self.record_bytes, np.uint8)
@@ -167,6 +172,15 @@ class Engine:
         check(self._lib.pir_engine_alloc_dev(self._h, nbytes, ctypes.byref(p)), "alloc_dev")
         return p.value
 
+    def free_dev(self, d_ptr):
+        check(self._lib.pir_engine_free_dev(self._h, d_ptr), "free_dev")
+
+    def set_party(self, party_index):
+        """Answer later queries as party `party_index` over the same resident shard
+        (server.partyIndex, src/c/server.h:16)."""
+        check(self._lib.pir_engine_set_party_index(self._h, int(party_index)), "set_party_index")
+        self.party_index = int(party_index)
+
     def h2d(self, d_ptr, host):
         h, hp = _buf(host)
         check(self._lib.pir_engine_memcpy_h2d(self._h, d_ptr, hp, h.size), "memcpy_h2d")
@@ -200,12 +214,19 @@ class Engine:
         keys = [bytes(k) for k in keys]
         nk = len(keys)
         d_k = self.alloc_dev(max(1, nk * self.key_len))
-        d_r = self.alloc_dev(max(1, nk * self.answer_bytes))
-        if nk:
-            self.h2d(d_k, b"".join(keys))
-        self.answer_stream_dev(d_k, nk, d_r)
-        self.sync()
-        return self.d2h(d_r, nk * self.answer_bytes).reshape(nk, self.num_rounds, self.record_bytes)
+        try:
+            d_r = self.alloc_dev(max(1, nk * self.answer_bytes))
+            try:
+                if nk:
+                    self.h2d(d_k, b"".join(keys))
+                self.answer_stream_dev(d_k, nk, d_r)
+                self.sync()
+                out = self.d2h(d_r, nk * self.answer_bytes)
+            finally:
+                self.free_dev(d_r)
+        finally:
+            self.free_dev(d_k)
+        return out.reshape(nk, self.num_rounds, self.record_bytes)
 
     @property
     def stream(self):

@@ -57,6 +57,11 @@ void pir_engine_destroy(pir_engine_t *e);
 int pir_engine_key_len(int num_parties, int log_num_records, int num_rounds);
 /* records (rows) held by this engine = 2^(n - G) */
 uint64_t pir_engine_num_rows(const pir_engine_t *e);
+/* answer later queries as party `party_index` (1-based) over the same shard: the reference's
+ * server.partyIndex (server.h:16), which only selects the root control bits of the DPF
+ * evaluation (dpf_tree.cpp:496-502).  Lets one resident shard serve every party's key in
+ * tests and benchmarks without a second copy of it. */
+int pir_engine_set_party_index(pir_engine_t *e, int party_index);
 
 /* ---- shard (device-resident; rows are this engine's partition, row 0 = its first) ---- */
 /* rows [row0, row0+nrows) from a host buffer with src_pitch bytes between rows */
@@ -119,6 +124,8 @@ void *pir_engine_stream(pir_engine_t *e);
 int pir_engine_sync(pir_engine_t *e);
 /* device scratch the caller may use for keys/results (freed with the engine) */
 int pir_engine_alloc_dev(pir_engine_t *e, size_t bytes, void **d_ptr);
+/* release a pir_engine_alloc_dev buffer before the engine is destroyed (waits for the device) */
+int pir_engine_free_dev(pir_engine_t *e, void *d_ptr);
 int pir_engine_memcpy_h2d(pir_engine_t *e, void *d_dst, const void *h_src, size_t bytes);
 int pir_engine_memcpy_d2h(pir_engine_t *e, void *h_dst, const void *d_src, size_t bytes);
 

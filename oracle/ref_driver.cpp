@@ -109,6 +109,36 @@ void* ref_server_new(int p, int party1, int n, int efs, int nq, const uint8_t* s
     return h;
 }
 
+// A reference server whose indexList rows point into a caller-owned contiguous N x efs shard
+// (e.g. a shared read-only file mapping: the all-cores CPU leg runs one process per core over
+// ONE copy of a 16 GiB shard).  The fields are those initializeServer sets (server.cpp:17-42);
+// only the row storage differs (the reference mallocs each row; the answer path reads rows
+// through indexList either way).  Free with ref_server_view_free.
+void* ref_server_view(int p, int party1, int n, int efs, int nq, const uint8_t* shard) {
+    set_tree_globals(p, n, efs, nq);
+    ref_srv* h = new ref_srv;
+    h->p = p; h->n = n; h->efs = efs; h->nq = nq;
+    size_t N = (size_t)1 << n;
+    h->s.ctx = EVP_CIPHER_CTX_new();
+    h->s.ctxThreads = (EVP_CIPHER_CTX**)malloc(sizeof(EVP_CIPHER_CTX*));
+    h->s.ctxThreads[0] = EVP_CIPHER_CTX_new();
+    h->s.partyIndex = party1;
+    h->s.indexList = (uint8_t**)malloc(N * sizeof(uint8_t*));
+    for (size_t i = 0; i < N; i++) h->s.indexList[i] = (uint8_t*)shard + i * efs;
+    h->s.isByzantine = 0;
+    h->s.numThreads = 1;
+    return h;
+}
+
+void ref_server_view_free(void* hv) {
+    ref_srv* h = (ref_srv*)hv;
+    EVP_CIPHER_CTX_free(h->s.ctx);
+    EVP_CIPHER_CTX_free(h->s.ctxThreads[0]);
+    free(h->s.ctxThreads);
+    free(h->s.indexList);
+    delete h;
+}
+
 // server.cpp:96-134; result is nq x efs
 void ref_server_answer(void* hv, const uint8_t* key, uint8_t* result) {
     ref_srv* h = (ref_srv*)hv;

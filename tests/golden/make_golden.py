@@ -178,14 +178,47 @@ def thread_defect():
                                  "thread0_c_nonzero": int((c_thr != 0).sum())})
 
 
+def fullsize():
+    """Reference answers at BASELINE sizes: configs[1] (2^20 x 1 KiB, p=2) itself, the C5 party
+    shape (p=8, NUM_ROUNDS=5) at 2^18 x 1 KiB and the C3 record size at 2^22 x 256 B.  The
+    shard INPUT is xorshift64 (the same generator as above, filled by the test oracle's C
+    loop for speed; its first bytes are checked against the Python definition here)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    assert np.array_equal(O.xorshift(SHARD_SEED, 4096), xorshift_bytes(SHARD_SEED, 4096))
+    cases = []
+    for (p, n, efs, nq, idx) in [(2, 20, 1024, 1, (1 << 20) // 3 + 7), (8, 18, 1024, 5, 77777),
+                                 (2, 22, 256, 1, (1 << 22) - 12345)]:
+        kl = REF.ref_key_len(p, n, nq)
+        fcw = final_cw(p, nq, 1, nq)
+        keys = np.zeros(p * kl, np.uint8)
+        REF.ref_gen_opt_dpf(n, U64(idx), ptr(fcw), p, nq, ptr(keys))
+        shard = O.xorshift(SHARD_SEED, (1 << n) * efs)
+        parties = sorted({0, 1, p - 1})
+        per = {}
+        for party in parties:
+            h = REF.ref_server_new(p, party + 1, n, efs, nq, ptr(shard), 0, 1)
+            res = np.zeros(nq * efs, np.uint8)
+            REF.ref_server_answer(ctypes.c_void_p(h), ptr(keys[party * kl:]), ptr(res))
+            REF.ref_server_free(ctypes.c_void_p(h))
+            per[str(party)] = {"key": keys[party * kl:(party + 1) * kl].tobytes().hex(),
+                               "answer": res.tobytes().hex()}
+        cases.append({"p": p, "n": n, "efs": efs, "nq": nq, "index": idx,
+                      "final_cw": fcw.tobytes().hex(), "shard_sha256": sha(shard),
+                      "parties": per})
+        print("fullsize case", p, n, efs, nq)
+    write("fullsize.json", {"shard_seed": SHARD_SEED, "cases": cases})
+
+
 if __name__ == "__main__":
     REF.ref_server_new.restype = ctypes.c_void_p
     REF.ref_blen.restype = ctypes.c_uint32
     for fn in (REF.ref_gf_mul, REF.ref_gf_pow, REF.ref_gf_inv):
         fn.restype = ctypes.c_uint8
-    what = sys.argv[1:] or ["prg", "gf", "dpf", "e2e", "thread"]
+    what = sys.argv[1:] or ["prg", "gf", "dpf", "e2e", "thread", "fullsize"]
     if "prg" in what: prg_kats()
     if "gf" in what: gf_kats()
     if "dpf" in what: dpf_and_answers()
     if "e2e" in what: e2e()
     if "thread" in what: thread_defect()
+    if "fullsize" in what: fullsize()

@@ -1,6 +1,7 @@
 """bench.py's CPU-baseline leg on a small shape (CPU only): the 1-core reference timing and the
-all-cores aggregate (worker processes, one reference server and one query each) agree on the
-answer with each other and with the plain-C oracle."""
+all-cores aggregate (worker processes over one shared read-only mapping of the shard, one
+reference server and one query each) agree on the answer with each other and with the plain-C
+oracle."""
 import ctypes
 import os
 import sys
@@ -14,7 +15,7 @@ sys.path.insert(0, ROOT)
 
 
 @pytest.mark.skipif(not os.path.exists(REF_SO), reason="oracle/_ref not built")
-def test_cpu_baseline_legs_agree(monkeypatch):
+def test_cpu_baseline_legs_agree(monkeypatch, tmp_path):
     import bench
     import _oracle as O
 
@@ -28,7 +29,11 @@ def test_cpu_baseline_legs_agree(monkeypatch):
     L.ref_gen_opt_dpf(n, ctypes.c_uint64(1234), P(fcw), p, nq, P(keys))
     shard = np.random.default_rng(7).integers(0, 256, (1 << n) * efs, dtype=np.uint8)
     want = O.answer(p, 1, n, efs, nq, keys[kl:].tobytes(), shard).reshape(nq, efs)
-    r = bench.cpu_baseline(keys[kl:].tobytes(), shard, n, efs, p, nq, want, budget_s=0.5)
+    path = str(tmp_path / "shard.bin")
+    shard.tofile(path)
+    assert bench._host_cores() == 2  # the share minus the GPU process's own core
+    r = bench.cpu_baseline(path, n, efs, p, nq, keys[kl:].tobytes(), want, 0.5,
+                           bench._host_cores())
     assert r["kind"] == "reference" and r["bit_exact_vs_gpu"]
     ac = r["all_cores"]
-    assert ac["cores"] == 3 and ac["answers_agree"] and ac["value"] > 0
+    assert ac["cores"] == 2 and ac["answers_agree"] and ac["value"] > 0

@@ -1,0 +1,157 @@
+"""BASELINE configs at full size on one MI355X, through the C ABI.
+
+  configs[1]  2^20 x 1 KiB, p=2        answers == the reference's own (tests/golden/fullsize.json)
+  configs[2]  2^24 x 256 B, 128 keys   PIR property for every key; batch == queue answers
+  configs[3]  2^27 x 1 KiB logical     one 128 GiB engine: PIR property; the 8 partition engines
+                                       of the split-shard layout (2^24 rows each) XOR to it
+  configs[4]  2^24 x 1 KiB, p=8, NR=5  per-round share property over several parties; the
+                                       encoded shards of all 8 servers, 2 dropped, decode
+
+The oracle cannot answer these sizes in a test's time, so the checks are the reference's own
+answers where it finishes here (golden), else size-independent properties of the protocol:
+ans_0 ^ ans_j == finalCW[r][j] * record (dpf_tree.cpp:142-274 key structure), XOR of
+partition answers == whole answer (linearity over rows), and erasure decode == the record
+(client.cpp:211-268).  One resident shard serves every party via pir_engine_set_party_index.
+"""
+import numpy as np
+import pytest
+
+import _oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pir():
+    import erasurecodedpir_amd as pir
+    pir.load()
+    return pir
+
+
+def _gf_table(c):
+    return np.array([O.gf_mul(c, x) for x in range(256)], np.uint8)
+
+
+@pytest.mark.parametrize("ci", range(3))
+def test_fullsize_golden(pir, ci):
+    """configs[1] itself, the C5 party shape (p=8, NR=5) at 2^18 x 1 KiB and 2^22 x 256 B:
+    GPU answers (single, queued) equal the reference's runOptimizedDPFTreeQuery answers."""
+    g = O.golden("fullsize.json")
+    case = g["cases"][ci]
+    p, n, efs, nq = case["p"], case["n"], case["efs"], case["nq"]
+    shard = O.xorshift(g["shard_seed"], (1 << n) * efs)
+    assert O.sha(shard) == case["shard_sha256"]
+    with pir.Engine(p, 1, n, efs, nq) as e:
+        e.set_shard(shard)
+        del shard
+        for party_s, ent in sorted(case["parties"].items()):
+            party = int(party_s)
+            e.set_party(party + 1)
+            key = bytes.fromhex(ent["key"])
+            assert e.answer(key).tobytes().hex() == ent["answer"], (p, n, efs, party)
+            q = e.answer_stream([key, key])
+            assert q[1].tobytes().hex() == ent["answer"], (p, n, efs, party)
+
+
+def test_c3_full_size_batch_128(pir):
+    """configs[2]: 2^24 x 256 B, 128 batched keys (distinct indices): every key's party-1 ^
+    party-2 answer is finalCW * record; the batched path equals the query queue."""
+    p, nq, n, efs, nk = 2, 1, 24, 256, 128
+    rng = np.random.default_rng(2024)
+    idxs = [int(i) for i in rng.choice(1 << n, nk, replace=False)]
+    idxs[0], idxs[1] = 0, (1 << n) - 1
+    fcw = O.final_cw(p, nq, 1)
+    keys = [pir.gen_keys(n, i, p, nq, fcw=fcw) for i in idxs]
+    tab = _gf_table(int(fcw[0]))
+    with pir.Engine(p, 1, n, efs, nq) as e:
+        e.fill_shard_random(0xC3)
+        a1 = e.answer_batch([k[0] for k in keys])
+        q1 = e.answer_stream([k[0] for k in keys[:16]])
+        e.set_party(2)
+        a2 = e.answer_batch([k[1] for k in keys])
+        recs = [e.shard_row(i) for i in idxs]
+    assert a1.shape == (nk, nq, efs)
+    for q in range(16):
+        assert np.array_equal(a1[q], q1[q]), q
+    bad = [q for q in range(nk) if not np.array_equal(a1[q][0] ^ a2[q][0], tab[recs[q]])]
+    assert not bad, bad
+
+
+def test_c4_single_engine_and_partitions(pir):
+    """configs[3] on one GPU: the 2^27 x 1 KiB logical shard as ONE engine (128 GiB of HBM),
+    PIR property; the 8 partition engines (log_num_partitions = 3, 2^24 rows each, created one
+    at a time over the same global rows) XOR to the whole answer, queued and single."""
+    p, nq, n, efs, G = 2, 1, 27, 1024, 3
+    fcw = O.final_cw(p, nq, 1)
+    idxs = [(1 << n) // 3 + 11, 5, (1 << n) - 2]
+    keys = [pir.gen_keys(n, i, p, nq, fcw=fcw) for i in idxs]
+    with pir.Engine(p, 1, n, efs, nq) as e:
+        e.fill_shard_random(0xC4)
+        full = e.answer_stream([k[0] for k in keys])
+        assert np.array_equal(e.answer(keys[0][0]), full[0])
+        e.set_party(2)
+        other = e.answer(keys[0][1])
+        rec = e.shard_row(idxs[0])
+    assert np.array_equal(full[0][0] ^ other[0], _gf_table(int(fcw[0]))[rec])
+    acc = np.zeros_like(full)
+    for part in range(1 << G):
+        with pir.Engine(p, 1, n, efs, nq, log_num_partitions=G, partition_index=part) as e:
+            e.fill_shard_random(0xC4)
+            acc ^= e.answer_stream([k[0] for k in keys])
+            if part == 0:
+                single0 = e.answer(keys[0][0])
+    assert np.array_equal(acc, full)
+    assert single0.any()
+
+
+def test_c5_full_size_round_shares(pir):
+    """configs[4] per-server shape: 2^24 x 1 KiB, p=8, NUM_ROUNDS=5 (k=5, r=2).  For every
+    round r and party j: ans_0[r] ^ ans_j[r] == finalCW[r][j] * record (queued and single)."""
+    p, nq, n, efs = 8, 5, 24, 1024
+    fcw = O.final_cw(p, nq, 1)
+    idxs = [(1 << n) // 3, 1234567]
+    keys = [pir.gen_keys(n, i, p, nq, fcw=fcw) for i in idxs]
+    ans = {}
+    with pir.Engine(p, 1, n, efs, nq) as e:
+        e.fill_shard_random(0xC5)
+        recs = [e.shard_row(i) for i in idxs]
+        for party in (0, 1, 4, 7):
+            e.set_party(party + 1)
+            ans[party] = e.answer_stream([k[party] for k in keys])
+            assert np.array_equal(e.answer(keys[1][party]), ans[party][1])
+    for q in range(len(idxs)):
+        for party in (1, 4, 7):
+            for r in range(nq):
+                cw = int(fcw[r * (p - 1) + party - 1])
+                assert np.array_equal(ans[0][q][r] ^ ans[party][q][r], _gf_table(cw)[recs[q]]), \
+                    (q, party, r)
+
+
+def test_c5_full_size_encode_drop_two_decode(pir):
+    """configs[4] end to end: 8 servers' erasure-coded 2^24 x 1 KiB shards (encode-across of
+    the reference's synthetic 2^26-file database on the GPU, client.cpp:16-33, 70-97), each
+    answers its key; servers 2 and 6 are dropped; the client decodes every record
+    (client.cpp:211-268)."""
+    from erasurecodedpir_amd import server as S
+    L, f, k, r = 26, 1024, 5, 2
+    S.setSystemParams(L, f, 1, k, r, 0, 1, 0, 0)
+    prm = S.params()
+    p, n, nq, efs = (prm["NUM_PARTIES"], prm["LOG_NUM_ENCODED_FILES"], prm["NUM_ROUNDS"],
+                     prm["ENCODED_FILE_SIZE_BYTES"])
+    assert (p, n, nq, efs) == (8, 24, 5, 1024)
+    encdb = -(-(1 << L) // k)
+    rows = [1, 2, encdb - 1, 777777]
+    fcw = O.final_cw(p, nq, 1)
+    keys = [pir.gen_keys(n, row, p, nq, fcw=fcw) for row in rows]
+    answers = []
+    with pir.Engine(p, 1, n, efs, nq) as e:
+        for party in range(p):
+            e.set_party(party + 1)
+            e.encode_across(1 << L, k)  # party q's shard: coefficients gf_pow(q, j)
+            answers.append(e.answer_stream([kk[party] for kk in keys]))
+    er = [0 if i in (2, 6) else 1 for i in range(p)]
+    for q, row in enumerate(rows):
+        kept = np.stack([answers[i][q] for i in range(p) if er[i]])
+        dec = S.assembleDPFTreeQueryResponses(er, kept)
+        want = np.arange(f, dtype=np.uint8) if row == 1 else np.full(f, row & 0xFF, np.uint8)
+        assert np.array_equal(dec, want), row
