@@ -60,6 +60,12 @@ CONFIGS = {
     "c5": (24, 1024, 8, 5, False, "configs[4] per-GPU server: 2^24 x 1 KiB shard, p=8 (k=5, r=2), NUM_ROUNDS=5"),
     "c4": (27, 1024, 2, 1, True, "configs[3]: one logical server, 2^27 x 1 KiB split over the GPUs, RCCL all-gather + XOR fold"),
 }
+# explicit-coefficient (polynomial / Hollanti) answers: a step = one query's NUM_ROUNDS
+# coefficient vectors (device-resident) scanned against the shard (server.cpp:321-371)
+COEF_CONFIGS = {
+    "ch": (24, 1024, 1, "polynomial (Hollanti) PIR: 2^24 x 1 KiB shard, 1 round, explicit coefficient vector"),
+    "ch3": (24, 1024, 3, "polynomial (Hollanti) PIR: 2^24 x 1 KiB shard, 3 rounds (k=3), explicit coefficient vectors"),
+}
 # batched configs: a step answers `batch` keys (distinct indices) against the shard
 BATCH_CONFIGS = {
     "c3b": (24, 256, 2, 1, 128, "configs[2]: 1 MI355X, one shard 2^24 x 256 B, 128 batched queries"),
@@ -383,7 +389,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default=None, choices=sorted(CONFIGS) + sorted(BATCH_CONFIGS),
+    ap.add_argument("--config", default=None,
+                    choices=sorted(CONFIGS) + sorted(BATCH_CONFIGS) + sorted(COEF_CONFIGS),
                     help="default: c24 on one GPU, c4 (split shard) on several")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=20.0,
@@ -417,6 +424,8 @@ def main():
     config = args.config or ("c24" if world == 1 else "c4")
     if config in BATCH_CONFIGS:
         return run_batch(args, ctx, config)
+    if config in COEF_CONFIGS:
+        return run_coefs(args, ctx, config)
     n_cfg, efs, p, nq, strong, workload = CONFIGS[config]
     g = log2_exact(world)
     n = n_cfg if strong else n_cfg + g  # logical tree depth
@@ -579,6 +588,51 @@ def extra_leg(ctx, pir, config, W, K, rng, single=True):
                                "note": "batch = 1: one launch per query"}
         res["queue_equals_one_at_a_time"] = bool(np.array_equal(m["answers"], m["singles"]))
     return res
+
+
+def run_coefs(args, ctx, config):
+    """Polynomial-PIR answers (answer_coefs_dev): each step scans one query's device-resident
+    coefficient vectors against the shard.  N = 1 only (replicas on more GPUs)."""
+    import erasurecodedpir_amd as pir
+    n, efs, nq, workload = COEF_CONFIGS[config]
+    N = 1 << n
+    eng = pir.Engine(2, 1, n, efs, nq, device=ctx.local)
+    eng.fill_shard_random(SHARD_SEED)
+    rng = np.random.default_rng(7)
+    K, W = args.steps, args.warmup
+    nkeys = max(2, min(K, 4))  # distinct queries, cycled
+    d_c = eng.alloc_dev(nkeys * nq * N)
+    d_r = eng.alloc_dev(K * nq * efs)
+    for q in range(nkeys):
+        eng.h2d(d_c + q * nq * N, rng.integers(0, 256, nq * N, dtype=np.uint8))
+    for i in range(W):
+        eng.answer_coefs_dev(d_c + (i % nkeys) * nq * N, N, 0, N, d_r)
+    dt = ctx.timed(eng, lambda: [eng.answer_coefs_dev(d_c + (i % nkeys) * nq * N, N, 0, N,
+                                                      d_r + i * nq * efs) for i in range(K)])
+    ms = dt / K * 1e3
+    # correctness at full size: one coefficient changed by x moves its round's answer by x*record
+    host = eng.d2h(d_c, nq * N).reshape(nq, N)
+    base = eng.answer_coefs(host)
+    i, x = N // 3, 0x35
+    host[nq - 1, i] ^= x
+    moved = eng.answer_coefs(host)
+    ok = bool(np.array_equal((base ^ moved)[nq - 1], _gf_table(x)[eng.shard_row(i)]))
+    eng.close()
+    gib = float(N) * efs / GIB
+    algo = float(N) * (efs + nq)  # shard + the query's coefficients
+    out = {"metric": METRIC, "value": round(gib / (ms / 1e3), 3), "unit": "GiB/s", "n_gpus": 1,
+           "steps": K, "warmup": W, "ms_per_step": r5(ms), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+           "config": {"workload": workload, "records": N, "record_bytes": efs, "num_rounds": nq,
+                      "step": "one query: interleave its coefficient vectors + GF(2^8) scan + reduce"},
+           "roofline": {"bound": "hbm", "kernel": "k_interleave_coefs + k_scan + k_reduce",
+                        "achieved": round(algo / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": None, "algorithmic_bytes_per_query": int(algo),
+                        "note": "wall time per query over the device work of all three launches"},
+           "parity": {"coefficient_linearity": ok}}
+    if ctx.rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def run_batch(args, ctx, config):

@@ -74,6 +74,8 @@ PROTOTYPES = {
     "pir_engine_answer": (_I, [_P, _P, _P]),
     "pir_engine_answer_slice": (_I, [_P, _P, _I, _I, _P]),
     "pir_engine_eval_all": (_I, [_P, _P, _P]),
+    "pir_engine_answer_coefs": (_I, [_P, ctypes.POINTER(_P), _U64, _U64, _P]),
+    "pir_engine_answer_coefs_dev": (_I, [_P, _P, _U64, _U64, _U64, _P, _P]),
     "pir_engine_answer_dev": (_I, [_P, _P, _P, _P]),
     "pir_engine_answer_batch_dev": (_I, [_P, _P, _I, _P, _P]),
     "pir_engine_answer_batch": (_I, [_P, _P, _I, _P]),
@@ -114,7 +116,38 @@ PROTOTYPES = {
     "encode_across_files_server": (None, [ctypes.POINTER(CClient), ctypes.POINTER(CServer)]),
     "assembleDPFTreeQueryResponses": (None, [ctypes.POINTER(CClient), _P,
                                              ctypes.POINTER(ctypes.POINTER(c_u8_p)), _P]),
+    "assembleHollantiResponses": (None, [ctypes.POINTER(CClient), _P,
+                                         ctypes.POINTER(ctypes.POINTER(c_u8_p)), _P]),
     "lagrangeInterpolationSemihonest": (None, [_P, ctypes.c_uint8, _P, ctypes.c_uint8, _P]),
+    "runHollantiQuery": (None, [ctypes.POINTER(CServer), ctypes.POINTER(c_u8_p),
+                                ctypes.POINTER(c_u8_p)]),
+    "runHollantiQueryThread": (None, [ctypes.POINTER(CServer), ctypes.POINTER(c_u8_p), _I, _I, _I,
+                                      ctypes.POINTER(c_u8_p)]),
+    "assembleHollantiQueryThreadResults": (None, [ctypes.POINTER(CServer),
+                                                  ctypes.POINTER(ctypes.POINTER(c_u8_p)), _I,
+                                                  ctypes.POINTER(c_u8_p)]),
+    "encode_within_files_server": (None, [ctypes.POINTER(CClient), ctypes.POINTER(CServer)]),
+    "runOptShamirDPFQueryThread": (None, [ctypes.POINTER(CServer), ctypes.POINTER(c_u8_p), _I, _I,
+                                          _I, ctypes.POINTER(c_u8_p)]),
+    "runOptimizedMultiPartyDPFQueryThread": (None, [ctypes.POINTER(CServer), _P, _I, _I,
+                                                    ctypes.POINTER(c_u8_p)]),
+    "runCDQueryThread": (None, [ctypes.POINTER(CServer), _P, _I, _I, ctypes.POINTER(c_u8_p)]),
+    "runWoodruffQueryThread": (None, [ctypes.POINTER(CServer), _P, _I, _I, _I,
+                                      ctypes.POINTER(c_u8_p)]),
+    "assembleShamirQueryThreadResults": (None, [ctypes.POINTER(CServer),
+                                                ctypes.POINTER(ctypes.POINTER(c_u8_p)), _I,
+                                                ctypes.POINTER(c_u8_p)]),
+    "assembleMultipartyDPFQueryThreadResults": (None, [ctypes.POINTER(CServer),
+                                                       ctypes.POINTER(ctypes.POINTER(c_u8_p)), _I,
+                                                       ctypes.POINTER(c_u8_p)]),
+    "assembleCDQueryThreadResults": (None, [ctypes.POINTER(CServer),
+                                            ctypes.POINTER(ctypes.POINTER(c_u8_p)), _I,
+                                            ctypes.POINTER(c_u8_p)]),
+    "assembleWoodruffQueryThreadResults": (None, [ctypes.POINTER(CServer),
+                                                  ctypes.POINTER(ctypes.POINTER(c_u8_p)), _I,
+                                                  ctypes.POINTER(c_u8_p)]),
+    "calcShamirDPFKeyLength": (_I, [_I]),
+    "calcShamirResponseLength": (_I, [_I, _I]),
     "pirSetDevice": (None, [_I]),
     "pirServerShardChanged": (None, [ctypes.POINTER(CServer)]),
 }
@@ -122,7 +155,8 @@ PROTOTYPES = {
 GLOBALS_INT = ["NUM_PARTIES", "NUM_FILES", "NUM_ENCODED_FILES", "LOG_NUM_ENCODED_FILES",
                "ENCODED_PAYLOAD_SIZE_BYTES", "ENCODED_FILE_SIZE_BYTES", "ENCODE_ACROSS",
                "NUM_ROUNDS", "RHO", "K", "T", "R", "B", "NUM_RESPONSES", "MODE", "IS_HERMITE",
-               "D", "MAC_SIZE_BYTES", "CHECK_MAC"]
+               "D", "MAC_SIZE_BYTES", "CHECK_MAC", "NUM_RSS_KEYS", "NUM_CD_KEYS", "WOODRUFF_M",
+               "WOODRUFF_D", "WOODRUFF_DERIVATIVE"]
 GLOBALS_U32 = ["LOG_NUM_FILES", "FILE_SIZE_BYTES", "PAYLOAD_SIZE_BYTES"]
 
 _lib = None

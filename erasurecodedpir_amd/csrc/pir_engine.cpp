@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/pir_engine.h"
+#include "pir_coefs.h"
 #include "pir_kernels.h"
 
 namespace {
@@ -116,6 +117,8 @@ struct pir_engine {
   uint8_t* d_result = nullptr;  // nq*efs (host-API staging)
   uint8_t* d_qscratch = nullptr;  // k_query super-tile tile inputs
   size_t qscratch_cap = 0;
+  uint8_t* d_coef_stage = nullptr;  // explicit-coefficient answers: host vectors staged here
+  size_t coef_stage_cap = 0;
   uint8_t* h_key = nullptr;     // pinned
   uint8_t* h_res = nullptr;     // pinned
   std::vector<DevBuf> user;     // pir_engine_alloc_dev
@@ -572,6 +575,40 @@ int answer_stream_locked(pir_engine* e, const uint8_t* d_keys, int nk, uint8_t* 
   return PIR_OK;
 }
 
+// Explicit-coefficient answer (server.cpp:321-382): out[a] = XOR_{i < nrows} src[a*pitch + i] *
+// shard[row0 + i].  The vectors are interleaved into the record-major share buffer, then the
+// same GF(2^8) scan + slab reduce as the 2-kernel DPF path; with a communicator, the partition
+// partials are combined like answers (all-gather + XOR fold).
+int answer_coefs_locked(pir_engine* e, const uint8_t* src, uint64_t pitch, uint64_t row0,
+                        uint64_t nrows, uint8_t* d_result, hipStream_t s) {
+  const auto& c = e->cfg;
+  const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
+  uint8_t* out = e->comm ? e->d_part : d_result;
+  e->ev = nullptr;
+  if (nrows == 0) {
+    HIP_TRY(hipMemsetAsync(out, 0, out_bytes, s));
+  } else {
+    const pir::ScanShape sh = pir::make_scan_shape(nrows, e->pitch, c.num_rounds, e->num_cus);
+    int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
+    if (rc) return rc;
+    HIP_TRY(pir::launch_interleave_coefs(src, pitch, nrows, c.num_rounds, e->nrp, e->d_c, s));
+    HIP_TRY(pir::launch_scan(sh, e->d_shard + row0 * e->pitch, nrows, e->d_c, e->d_slabs, false, s));
+    HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, out, s));
+  }
+  if (e->comm) {
+    RCCL_TRY(ncclAllGather(e->d_part, e->d_gather, out_bytes, ncclUint8, e->comm, s));
+    HIP_TRY(pir::launch_xor_fold(e->d_gather, e->nranks, out_bytes, d_result, s));
+  }
+  return PIR_OK;
+}
+
+int check_rows(const pir_engine* e, uint64_t row0, uint64_t nrows) {
+  if (row0 > e->rows || nrows > e->rows - row0)
+    return fail(PIR_EINVAL, "rows [%llu,%llu) beyond the %llu held", (unsigned long long)row0,
+                (unsigned long long)(row0 + nrows), (unsigned long long)e->rows);
+  return PIR_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -676,7 +713,8 @@ void pir_engine_destroy(pir_engine_t* e) {
                   (void*)e->nodes.s[0], (void*)e->nodes.s[1], (void*)e->nodes.t[0],
                   (void*)e->nodes.t[1], (void*)e->d_c, (void*)e->d_slabs, (void*)e->d_part,
                   (void*)e->d_gather, (void*)e->d_result, (void*)e->d_cb, (void*)e->d_gtmp,
-                  (void*)e->d_bpart, (void*)e->d_bgather, (void*)e->d_qscratch, (void*)e->bnodes.s[0],
+                  (void*)e->d_bpart, (void*)e->d_bgather, (void*)e->d_qscratch, (void*)e->d_coef_stage,
+                  (void*)e->bnodes.s[0],
                   (void*)e->bnodes.s[1], (void*)e->bnodes.t[0], (void*)e->bnodes.t[1]})
     if (p) (void)hipFree(p);
   for (auto& b : e->user) (void)hipFree(b.p);
@@ -872,6 +910,47 @@ int pir_engine_answer(pir_engine_t* e, const uint8_t* key, uint8_t* result) {
   memcpy(e->h_key, key, e->key_len);
   HIP_TRY(hipMemcpyAsync(e->d_key_raw, e->h_key, e->key_len, hipMemcpyHostToDevice, e->stream));
   int rc = ws_release(e, e->stream, answer_dev_locked(e, e->d_key_raw, e->d_result, e->stream));
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(e->h_res, e->d_result, out_bytes, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memcpy(result, e->h_res, out_bytes);
+  return PIR_OK;
+}
+
+int pir_engine_answer_coefs_dev(pir_engine_t* e, const uint8_t* d_coefs, uint64_t coef_pitch,
+                                uint64_t row0, uint64_t nrows, uint8_t* d_result, void* stream) {
+  if (!e || !d_result || (!d_coefs && nrows)) return fail(PIR_EINVAL, "null argument");
+  if (int rc = check_rows(e, row0, nrows)) return rc;
+  if (e->cfg.num_rounds > 1 && coef_pitch < row0 + nrows)
+    return fail(PIR_EINVAL, "coef_pitch %llu < %llu rows", (unsigned long long)coef_pitch,
+                (unsigned long long)(row0 + nrows));
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  if (int rc = ws_acquire(e, s)) return rc;
+  return ws_release(e, s, answer_coefs_locked(e, d_coefs + row0, coef_pitch, row0, nrows,
+                                              d_result, s));
+}
+
+int pir_engine_answer_coefs(pir_engine_t* e, const uint8_t* const* coefs, uint64_t row0,
+                            uint64_t nrows, uint8_t* result) {
+  if (!e || !result || (!coefs && nrows)) return fail(PIR_EINVAL, "null argument");
+  if (int rc = check_rows(e, row0, nrows)) return rc;
+  const auto& c = e->cfg;
+  for (int a = 0; a < c.num_rounds && nrows; ++a)
+    if (!coefs[a]) return fail(PIR_EINVAL, "null coefficient vector %d", a);
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(c.device));
+  const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
+  if (int rc = ws_acquire(e, e->stream)) return rc;
+  int rc = ensure_buf(&e->d_coef_stage, &e->coef_stage_cap,
+                      std::max<size_t>(1, (size_t)c.num_rounds * nrows));
+  if (rc) return rc;
+  for (int a = 0; a < c.num_rounds && nrows; ++a)  // only the rows answered travel
+    HIP_TRY(hipMemcpyAsync(e->d_coef_stage + (size_t)a * nrows, coefs[a] + row0, nrows,
+                           hipMemcpyHostToDevice, e->stream));
+  rc = ws_release(e, e->stream, answer_coefs_locked(e, e->d_coef_stage, nrows, row0, nrows,
+                                                    e->d_result, e->stream));
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(e->h_res, e->d_result, out_bytes, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));

@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <random>
 #include <utility>
 #include <vector>
 
@@ -37,6 +38,11 @@ int IS_HERMITE = 0;
 int D = 0;
 int MAC_SIZE_BYTES = 32;
 int CHECK_MAC = 0;
+int NUM_RSS_KEYS = 0;  // params.cpp:39-46 defaults; their modes are not served
+int NUM_CD_KEYS = 0;
+int WOODRUFF_M = 0;
+int WOODRUFF_D = 0;
+int WOODRUFF_DERIVATIVE = 0;
 }
 
 namespace {
@@ -71,11 +77,17 @@ ShimState* state_of(server* s) {
   return static_cast<ShimState*>(s->ctx);
 }
 
+[[noreturn]] void out_of_scope(const char* fn, const char* mode) {
+  fprintf(stderr, "pir shim: %s (%s mode) is outside the tree-DPF engine's scope\n", fn, mode);
+  abort();
+}
+
 // Make sure the engine matches the current globals / nq and holds the current indexList.
 pir_engine_t* engine_for(server* s, ShimState* st, int nq) {
   pir_engine_config c{};
   c.device = device_default();
-  c.num_parties = NUM_PARTIES;
+  // the party count only sizes DPF keys; polynomial-PIR setups may have p < 2 or > 17
+  c.num_parties = NUM_PARTIES < 2 ? 2 : (NUM_PARTIES > PIR_MAX_PARTIES ? PIR_MAX_PARTIES : NUM_PARTIES);
   c.party_index = s->partyIndex;
   c.log_num_records = LOG_NUM_ENCODED_FILES;
   c.record_bytes = (uint32_t)ENCODED_FILE_SIZE_BYTES;
@@ -250,6 +262,51 @@ void assembleDPFTreeQueryResponses(client* c, uint8_t* erasureIndexList, uint8_t
   memcpy(output, acc.data(), FILE_SIZE_BYTES);
 }
 
+// client.cpp:499-552 (semi-honest, B == 0): the polynomial-PIR decode.  Round i peels the parts
+// recovered in earlier rounds off the shares (gf_pow(point, K + T - 1 + i - b)), then reads
+// coefficients K+T+RHO-2-q (q < RHO) of the degree-(K+T+RHO-2) interpolant at every byte
+// position into part K-1-i-q; one Vandermonde inverse per round.  output = FILE_SIZE_BYTES.
+void assembleHollantiResponses(client* c, uint8_t* erasureIndexList, uint8_t*** responses,
+                               uint8_t* output) {
+  (void)c;
+  if (B > 0) {
+    fprintf(stderr, "pir shim: malicious (B > 0) decoding is outside the engine's scope\n");
+    abort();
+  }
+  const int nr = NUM_PARTIES - R, efs = ENCODED_FILE_SIZE_BYTES, deg = K + T + RHO - 2;
+  const int m = deg + 1;
+  if (nr < m) {
+    fprintf(stderr, "pir shim: %d responses cannot decode degree %d\n", nr, deg);
+    abort();
+  }
+  std::vector<uint8_t> acc((size_t)K * efs, 0), pts(nr), sh((size_t)nr);
+  for (int i = 0; i < NUM_ROUNDS; ++i) {
+    int cur = 1;
+    for (int j = 0; j < nr; ++j) {
+      while (!erasureIndexList[cur - 1]) ++cur;
+      pts[j] = (uint8_t)cur++;
+    }
+    const std::vector<uint8_t> inv = vandermonde_inverse(pts.data(), m);
+    std::vector<uint8_t> peel((size_t)nr * i);
+    for (int j = 0; j < nr; ++j)
+      for (int b = 0; b < i; ++b) peel[(size_t)j * i + b] = gf_pow_h(pts[j], K + T - 1 + i - b);
+    for (int a = 0; a < efs; ++a) {
+      for (int j = 0; j < nr; ++j) {
+        uint8_t v = responses[j][i][a];
+        for (int b = 0; b < i; ++b)
+          v ^= gf_mul_h(acc[(size_t)(K - 1 - b) * efs + a], peel[(size_t)j * i + b]);
+        sh[j] = v;
+      }
+      for (int q = 0; q < RHO; ++q) {
+        const int row = deg - q, dst = K - 1 - i - q;
+        uint8_t v = 0;
+        for (int j = 0; j < m; ++j) v ^= gf_mul_h(sh[j], inv[(size_t)row * m + j]);
+        if (dst >= 0) acc[(size_t)dst * efs + a] = v;
+      }
+    }
+  }
+  memcpy(output, acc.data(), FILE_SIZE_BYTES);
+}
 
 void pirSetDevice(int device) { g_device = device; }
 
@@ -261,15 +318,21 @@ int calcOptimizedDPFTreeKeyLength(int p, int log_domainSize, int numQueries) {
   return pir_engine_key_len(p, log_domainSize, numQueries);
 }
 
-// params.cpp:467-512 with setModeParams(Tree) (params.cpp:414-418)
+// params.cpp:467-512 with setModeParams(Tree) (params.cpp:414-418) or setModeParams(Hollanti)
+// (params.cpp:430-433); the other modes (multiparty, Shamir, CD, Woodruff, Goldberg) abort
 void setSystemParams(int logNumFiles, int fileSizeBytes, int t, int k, int r, int b, int rho,
                      int checkMac, int mode) {
-  if (mode != 0) {
-    fprintf(stderr, "pir shim: mode %d is outside the tree-DPF engine's scope\n", mode);
+  if (mode != 0 && mode != 3) {
+    fprintf(stderr, "pir shim: mode %d is outside the engine's scope (tree = 0, Hollanti = 3)\n",
+            mode);
     abort();
   }
-  if (t != 1) {  // params.cpp:415 assert(T == 1)
+  if (mode == 0 && t != 1) {  // params.cpp:415 assert(T == 1)
     fprintf(stderr, "pir shim: tree mode requires t == 1 (got %d)\n", t);
+    abort();
+  }
+  if (mode == 3 && checkMac) {
+    fprintf(stderr, "pir shim: CheckMAC setups are outside the engine's scope\n");
     abort();
   }
   RHO = rho; K = k; T = t; R = r; B = b;
@@ -279,18 +342,35 @@ void setSystemParams(int logNumFiles, int fileSizeBytes, int t, int k, int r, in
   FILE_SIZE_BYTES = (uint32_t)fileSizeBytes;
   CHECK_MAC = checkMac;
   MODE = mode;
-  NUM_PARTIES = K + R + T + 2 * B + (RHO - 1);
-  ENCODE_ACROSS = 1;
+  NUM_PARTIES = K + R + T + 2 * B + (RHO - 1);  // the same sum for both modes
+  ENCODE_ACROSS = mode == 0 ? 1 : 0;
   NUM_RESPONSES = NUM_PARTIES - R;
-  LOG_NUM_ENCODED_FILES = ceil_log2((NUM_FILES + k - 1) / k);
-  NUM_ENCODED_FILES = 1 << LOG_NUM_ENCODED_FILES;
-  ENCODED_PAYLOAD_SIZE_BYTES = (int)FILE_SIZE_BYTES;
-  ENCODED_FILE_SIZE_BYTES = (int)FILE_SIZE_BYTES;
-  if (CHECK_MAC) {
-    FILE_SIZE_BYTES += MAC_SIZE_BYTES;
-    ENCODED_FILE_SIZE_BYTES += MAC_SIZE_BYTES;
+  if (ENCODE_ACROSS) {
+    LOG_NUM_ENCODED_FILES = ceil_log2((NUM_FILES + k - 1) / k);
+    NUM_ENCODED_FILES = 1 << LOG_NUM_ENCODED_FILES;
+    ENCODED_PAYLOAD_SIZE_BYTES = (int)FILE_SIZE_BYTES;
+    ENCODED_FILE_SIZE_BYTES = (int)FILE_SIZE_BYTES;
+    if (CHECK_MAC) {
+      FILE_SIZE_BYTES += MAC_SIZE_BYTES;
+      ENCODED_FILE_SIZE_BYTES += MAC_SIZE_BYTES;
+    }
+  } else {  // params.cpp:496-507: every file is split into K parts of ceil(f / K) bytes
+    NUM_ENCODED_FILES = NUM_FILES;
+    LOG_NUM_ENCODED_FILES = logNumFiles;
+    ENCODED_PAYLOAD_SIZE_BYTES = (int)((PAYLOAD_SIZE_BYTES + k - 1) / k);
+    ENCODED_FILE_SIZE_BYTES = (int)((FILE_SIZE_BYTES + k - 1) / k);
   }
   NUM_ROUNDS = (K == 1) ? 1 : K / RHO;
+}
+
+// utils.cpp:131-143
+int calcShamirDPFKeyLength(int log_domainSize) {
+  const int x = log_domainSize / 2 + (log_domainSize % 2 != 0), y = log_domainSize - x;
+  return (1 << x) + (1 << y);
+}
+
+int calcShamirResponseLength(int log_domainSize, int fileSizeBytes) {
+  return (calcShamirDPFKeyLength(log_domainSize) + 2) * fileSizeBytes;
 }
 
 void freeParams(void) {}
@@ -357,6 +437,98 @@ void assemblDPFTreeQueryThreadResults(server* s, uint8_t*** in, int numThreads, 
   }
 }
 
+// ---- polynomial (Hollanti) PIR: explicit coefficients, scanned on the engine ----------------
+// server.cpp:321-343: random answers for a Byzantine server, else the scan of every row
+void runHollantiQuery(server* s, uint8_t** key, uint8_t** result) {
+  ShimState* st = state_of(s);
+  const size_t efs = (size_t)ENCODED_FILE_SIZE_BYTES;
+  if (s->isByzantine) {  // gen_rand_bytes (server.cpp:329-332)
+    static std::mutex rmu;
+    static std::mt19937_64 rng{std::random_device{}()};
+    std::lock_guard<std::mutex> lk(rmu);
+    for (int a = 0; a < NUM_ROUNDS; ++a)
+      for (size_t j = 0; j < efs; ++j) result[a][j] = (uint8_t)rng();
+    return;
+  }
+  std::lock_guard<std::mutex> lk(st->mu);
+  pir_engine_t* e = engine_for(s, st, NUM_ROUNDS);
+  std::vector<uint8_t> out((size_t)NUM_ROUNDS * efs);
+  if (pir_engine_answer_coefs(e, key, 0, (uint64_t)NUM_ENCODED_FILES, out.data()) != PIR_OK)
+    die("runHollantiQuery");
+  for (int a = 0; a < NUM_ROUNDS; ++a) memcpy(result[a], out.data() + a * efs, efs);
+}
+
+// server.cpp:345-371: rows [startIndex, endIndex) (both of the reference's branches compute the
+// honest answer)
+void runHollantiQueryThread(server* s, uint8_t** keys, int threadNum, int startIndex, int endIndex,
+                            uint8_t** result) {
+  (void)threadNum;
+  ShimState* st = state_of(s);
+  if (startIndex < 0 || endIndex < startIndex || endIndex > NUM_ENCODED_FILES) {
+    fprintf(stderr, "pir shim: rows [%d,%d) outside [0,%d)\n", startIndex, endIndex,
+            NUM_ENCODED_FILES);
+    abort();
+  }
+  std::lock_guard<std::mutex> lk(st->mu);
+  pir_engine_t* e = engine_for(s, st, NUM_ROUNDS);
+  const size_t efs = (size_t)ENCODED_FILE_SIZE_BYTES;
+  std::vector<uint8_t> out((size_t)NUM_ROUNDS * efs);
+  if (pir_engine_answer_coefs(e, keys, (uint64_t)startIndex, (uint64_t)(endIndex - startIndex),
+                              out.data()) != PIR_OK)
+    die("runHollantiQueryThread");
+  for (int a = 0; a < NUM_ROUNDS; ++a) memcpy(result[a], out.data() + a * efs, efs);
+}
+
+// the reference's per-thread XOR folds: `rows` output rows of `len` bytes
+static void xor_fold(uint8_t*** in, int numThreads, uint8_t** out, int rows, size_t len) {
+  for (int a = 0; a < rows; ++a) {
+    memset(out[a], 0, len);
+    for (int t = 0; t < numThreads; ++t)
+      for (size_t j = 0; j < len; ++j) out[a][j] ^= in[t][a][j];
+  }
+}
+
+void assembleHollantiQueryThreadResults(server* s, uint8_t*** in, int numThreads, uint8_t** out) {
+  (void)s;  // server.cpp:373-382
+  xor_fold(in, numThreads, out, NUM_ROUNDS, (size_t)ENCODED_FILE_SIZE_BYTES);
+}
+
+void assembleShamirQueryThreadResults(server* s, uint8_t*** in, int numThreads, uint8_t** out) {
+  (void)s;  // server.cpp:304-319
+  xor_fold(in, numThreads, out, NUM_ROUNDS,
+           (size_t)calcShamirResponseLength(LOG_NUM_ENCODED_FILES, ENCODED_FILE_SIZE_BYTES));
+}
+
+void assembleMultipartyDPFQueryThreadResults(server* s, uint8_t*** in, int numThreads,
+                                             uint8_t** out) {
+  (void)s;  // server.cpp:432-441
+  xor_fold(in, numThreads, out, NUM_RSS_KEYS, (size_t)ENCODED_FILE_SIZE_BYTES);
+}
+
+void assembleCDQueryThreadResults(server* s, uint8_t*** in, int numThreads, uint8_t** out) {
+  (void)s;  // server.cpp:494-503
+  xor_fold(in, numThreads, out, NUM_CD_KEYS, (size_t)ENCODED_FILE_SIZE_BYTES);
+}
+
+void assembleWoodruffQueryThreadResults(server* s, uint8_t*** in, int numThreads, uint8_t** out) {
+  (void)s;  // server.cpp:647-665
+  xor_fold(in, numThreads, out, WOODRUFF_DERIVATIVE ? WOODRUFF_M + 1 : 1,
+           (size_t)ENCODED_FILE_SIZE_BYTES);
+}
+
+void runOptShamirDPFQueryThread(server*, uint8_t**, int, int, int, uint8_t**) {
+  out_of_scope("runOptShamirDPFQueryThread", "Shamir");
+}
+void runOptimizedMultiPartyDPFQueryThread(server*, uint8_t*, int, int, uint8_t**) {
+  out_of_scope("runOptimizedMultiPartyDPFQueryThread", "multiparty DPF");
+}
+void runCDQueryThread(server*, uint8_t*, int, int, uint8_t**) {
+  out_of_scope("runCDQueryThread", "covering-design");
+}
+void runWoodruffQueryThread(server*, uint8_t*, int, int, int, uint8_t**) {
+  out_of_scope("runWoodruffQueryThread", "Woodruff");
+}
+
 // client.cpp:16-33 (synthetic DB; MAC tags are outside this engine's scope)
 void initialize_client(client* c, uint8_t log_num_files, uint32_t file_size_bytes) {
   (void)file_size_bytes;
@@ -396,6 +568,31 @@ void encode_across_files_server(client* c, server* s) {
       if (src >= NUM_FILES) continue;
       const uint8_t* f = c->unencoded_files[src];
       for (int b = 0; b < efs; ++b) row[b] ^= gf_mul_h(f[b], coef[j]);
+    }
+  }
+  if (s->ctx) static_cast<ShimState*>(s->ctx)->dirty = true;
+}
+
+// client.cpp:43-56, 99-103: row i of party q = XOR_{j<K} gf_pow(q, j) * part j of file i, where
+// part j = bytes [j*EFS, (j+1)*EFS) of the file zero-padded to K*EFS (encodeMat[j][q-1] of
+// gen_encode_matrix, coding.cpp:64-70).  One 256-entry product table per coefficient.
+void encode_within_files_server(client* c, server* s) {
+  if (IS_HERMITE) out_of_scope("encode_within_files_server (Hermite rows)", "Shamir");
+  const int efs = ENCODED_FILE_SIZE_BYTES;
+  std::vector<uint8_t> tab((size_t)K * 256);
+  for (int j = 0; j < K; ++j) {
+    const uint8_t cj = gf_pow_h((uint8_t)s->partyIndex, j);
+    for (int x = 0; x < 256; ++x) tab[(size_t)j * 256 + x] = gf_mul_h((uint8_t)x, cj);
+  }
+  for (int i = 0; i < NUM_ENCODED_FILES; ++i) {
+    uint8_t* row = s->indexList[i];
+    const uint8_t* f = c->unencoded_files[i];
+    for (int j = 0; j < K; ++j) {
+      const uint8_t* t = &tab[(size_t)j * 256];
+      for (int b = 0; b < efs; ++b) {
+        const long src = (long)j * efs + b;
+        if (src < (long)FILE_SIZE_BYTES) row[b] ^= t[f[src]];
+      }
     }
   }
   if (s->ctx) static_cast<ShimState*>(s->ctx)->dirty = true;

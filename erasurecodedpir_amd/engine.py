@@ -158,6 +158,23 @@ class Engine:
               "pir_engine_answer_slice")
         return out
 
+    def answer_coefs(self, coefs, row0=0, nrows=None):
+        """Explicit-coefficient answer (runHollantiQuery[Thread], src/c/server.cpp:321-371):
+        coefs is (num_rounds, rows) uint8 -- coefficient of engine row r in round a at
+        coefs[a][r]; rows [row0, row0 + nrows) are answered.  (num_rounds, record_bytes)."""
+        c = np.ascontiguousarray(np.asarray(coefs, np.uint8).reshape(self.num_rounds, -1))
+        nrows = c.shape[1] - row0 if nrows is None else nrows
+        ptrs = (ctypes.c_void_p * self.num_rounds)(*[c[a].ctypes.data for a in range(self.num_rounds)])
+        out = np.empty((self.num_rounds, self.record_bytes), np.uint8)
+        check(self._lib.pir_engine_answer_coefs(self._h, ptrs, row0, nrows,
+                                                out.ctypes.data_as(ctypes.c_void_p)),
+              "pir_engine_answer_coefs")
+        return out
+
+    def answer_coefs_dev(self, d_coefs, coef_pitch, row0, nrows, d_result, stream=None):
+        check(self._lib.pir_engine_answer_coefs_dev(self._h, d_coefs, coef_pitch, row0, nrows,
+                                                    d_result, stream), "answer_coefs_dev")
+
     def eval_all(self, key):
         """(num_rounds, rows) DPF shares dataShare[a][i]."""
         k, kp = self._check_key(key)

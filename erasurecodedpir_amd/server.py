@@ -77,6 +77,26 @@ class Server:
                                                  numThreads, _row_ptrs(out))
         return out
 
+    def runHollantiQuery(self, keys):
+        """keys: (NUM_ROUNDS, NUM_ENCODED_FILES) coefficient vectors (server.cpp:321-343)."""
+        return self._hollanti(keys, None)
+
+    def runHollantiQueryThread(self, keys, threadNum, startIndex, endIndex):
+        """Rows [startIndex, endIndex) (server.cpp:345-371)."""
+        return self._hollanti(keys, (threadNum, startIndex, endIndex))
+
+    def _hollanti(self, keys, thread):
+        efs = _lib.global_int("ENCODED_FILE_SIZE_BYTES")
+        nq = _lib.global_int("NUM_ROUNDS")
+        k = np.ascontiguousarray(np.asarray(keys, np.uint8).reshape(nq, -1))
+        out = np.zeros((nq, efs), np.uint8)
+        kp = _row_ptrs(k)
+        if thread is None:
+            self._lib.runHollantiQuery(ctypes.byref(self.s), kp, _row_ptrs(out))
+        else:
+            self._lib.runHollantiQueryThread(ctypes.byref(self.s), kp, *thread, _row_ptrs(out))
+        return out
+
     def freeServer(self):
         if self.s.ctx:
             self._lib.freeServer(ctypes.byref(self.s))
@@ -103,6 +123,25 @@ def assemblDPFTreeQueryThreadResults(server, parts):
     return out
 
 
+def assembleHollantiQueryThreadResults(server, parts):
+    """parts: (numThreads, NUM_ROUNDS, EFS) -> (NUM_ROUNDS, EFS) (src/c/server.cpp:373-382)."""
+    return _assemble("assembleHollantiQueryThreadResults", server, parts)
+
+
+def _assemble(fn, server, parts):
+    parts = np.ascontiguousarray(parts, dtype=np.uint8)
+    T, nq, efs = parts.shape
+    ins = (ctypes.POINTER(c_u8_p) * T)()
+    keep = []
+    for t in range(T):
+        rp = _row_ptrs(parts[t])
+        keep.append(rp)
+        ins[t] = ctypes.cast(rp, ctypes.POINTER(c_u8_p))
+    out = np.zeros((nq, efs), np.uint8)
+    getattr(_lib.load(), fn)(ctypes.byref(server.s), ins, T, _row_ptrs(out))
+    return out
+
+
 class Client:
     """The synthetic-DB client of src/c/client.cpp:16-41 (server setup path)."""
 
@@ -113,6 +152,9 @@ class Client:
 
     def encode_across_files_server(self, server):
         self._lib.encode_across_files_server(ctypes.byref(self.c), ctypes.byref(server.s))
+
+    def encode_within_files_server(self, server):
+        self._lib.encode_within_files_server(ctypes.byref(self.c), ctypes.byref(server.s))
 
     def assembleDPFTreeQueryResponses(self, erasure, responses):
         """Client decode (client.cpp:211-268); see the module function of the same name."""
@@ -139,4 +181,21 @@ def assembleDPFTreeQueryResponses(erasure, responses, c=None):
     cl = c if c is not None else CClient()
     lib.assembleDPFTreeQueryResponses(ctypes.byref(cl), er.ctypes.data_as(ctypes.c_void_p), outer,
                                       out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+def assembleHollantiResponses(erasure, responses, c=None):
+    """Client decode of one polynomial (Hollanti) query (client.cpp:499-552) under the current
+    setSystemParams(mode 3): responses = [NUM_PARTIES - R][NUM_ROUNDS][EFS]."""
+    lib = _lib.load()
+    prm = params()
+    nr, nq, efs = prm["NUM_PARTIES"] - prm["R"], prm["NUM_ROUNDS"], prm["ENCODED_FILE_SIZE_BYTES"]
+    resp = np.ascontiguousarray(np.asarray(responses, np.uint8).reshape(nr, nq, efs))
+    er = np.ascontiguousarray(np.asarray(erasure, np.uint8))
+    rows = [(c_u8_p * nq)(*[resp[j, i].ctypes.data_as(c_u8_p) for i in range(nq)]) for j in range(nr)]
+    outer = (ctypes.POINTER(c_u8_p) * nr)(*[ctypes.cast(r, ctypes.POINTER(c_u8_p)) for r in rows])
+    out = np.zeros(_lib.global_int("FILE_SIZE_BYTES"), np.uint8)
+    cl = c if c is not None else CClient()
+    lib.assembleHollantiResponses(ctypes.byref(cl), er.ctypes.data_as(ctypes.c_void_p), outer,
+                                  out.ctypes.data_as(ctypes.c_void_p))
     return out

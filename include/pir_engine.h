@@ -14,6 +14,7 @@
  *   pir_engine_answer_slice          runOptimizedDPFTreeQueryThread (intended semantics)
  *                                                                           server.cpp:505-549
  *   pir_engine_eval_all              evalAllOptimizedDPF                    dpf_tree.cpp:473-598
+ *   pir_engine_answer_coefs[_dev]    runHollantiQuery / ...Thread           server.cpp:321-371
  *   pir_engine_key_len               calcOptimizedDPFTreeKeyLength          utils.cpp:85-90
  *   pir_comm_* + partitions          (new) split-shard across GPUs, XOR all-reduce over RCCL
  */
@@ -91,6 +92,17 @@ int pir_engine_answer(pir_engine_t *e, const uint8_t *key, uint8_t *result);
 /* partial answer over the engine rows [t*R/T, (t+1)*R/T), R = rows held, T a power of 2 */
 int pir_engine_answer_slice(pir_engine_t *e, const uint8_t *key, int thread_num,
                             int num_threads, uint8_t *result);
+/* ---- explicit-coefficient answers: the Hollanti/Goldberg polynomial-PIR server scan
+ *      (runHollantiQuery / runHollantiQueryThread, server.cpp:321-371) -- no DPF, the client
+ *      sends one coefficient vector per round ----
+ * result[a] = XOR_{r in [row0, row0+nrows)} coefs[a][r] * shard row r over GF(2^8)/0x11d, for
+ * a < num_rounds; coefs[a] is indexed by engine row (num_rounds host pointers).  Always the
+ * honest answer: the reference's Thread variant ignores isByzantine (server.cpp:353-369). */
+int pir_engine_answer_coefs(pir_engine_t *e, const uint8_t *const *coefs, uint64_t row0,
+                            uint64_t nrows, uint8_t *result);
+/* device form: round a's coefficient of engine row r at d_coefs[a * coef_pitch + r] */
+int pir_engine_answer_coefs_dev(pir_engine_t *e, const uint8_t *d_coefs, uint64_t coef_pitch,
+                                uint64_t row0, uint64_t nrows, uint8_t *d_result, void *stream);
 /* DPF shares of this engine's rows: out[a*R + i] (dataShare[a][i]) */
 int pir_engine_eval_all(pir_engine_t *e, const uint8_t *key, uint8_t *out);
 

@@ -11,7 +11,11 @@
  *                                      partial answer over rows [t*N/T,(t+1)*N/T); the reference
  *                                      body is defective)
  *   assemblDPFTreeQueryThreadResults   server.h:53,     server.cpp:553-562
- *   setSystemParams / freeParams       params.h:63-64,  params.cpp:467-642 (tree mode only)
+ *   setSystemParams / freeParams       params.h:63-64,  params.cpp:467-642 (tree and Hollanti
+ *                                      modes; the others abort)
+ *   runHollantiQuery[Thread], assemble*QueryThreadResults, the other modes' entry points (abort)
+ *                                      server.h:39-53,  server.cpp:304-665
+ *   encode_within_files_server         client.h:29,     client.cpp:93-110
  *   the sizing globals                 params.h:9-33
  *   client / initialize_client / free_client / encode_across_files_server
  *                                      client.h:15-28,  client.cpp:16-41, :70-97 (server setup
@@ -71,6 +75,13 @@ extern int IS_HERMITE;
 extern int D;
 extern int MAC_SIZE_BYTES;
 extern int CHECK_MAC;
+/* globals of the other PIR modes (params.h:39-54), read by the Go mode handlers
+ * (src/server_util/{multiparty,cd732,woodruff}.go); those modes are not served (see below) */
+extern int NUM_RSS_KEYS;
+extern int NUM_CD_KEYS;
+extern int WOODRUFF_M;
+extern int WOODRUFF_D;
+extern int WOODRUFF_DERIVATIVE;
 
 void setSystemParams(int logNumFiles, int fileSizeBytes, int t, int k, int r, int b, int rho,
                      int checkMac, int mode);
@@ -85,14 +96,50 @@ void runOptimizedDPFTreeQueryThread(server *s, uint8_t *key, int threadNum, int 
                                     uint8_t **result);
 void assemblDPFTreeQueryThreadResults(server *s, uint8_t ***in, int numThreads, uint8_t **out);
 
+/* ---- polynomial (Hollanti/Goldberg, mode 3) PIR: the explicit-coefficient scan on the engine
+ *      (server.h:39,44,51; server.cpp:321-382).  key[k] = the NUM_ROUNDS coefficient vectors of
+ *      NUM_ENCODED_FILES bytes; result[k] = ENCODED_FILE_SIZE_BYTES. ---- */
+void runHollantiQuery(server *s, uint8_t **key, uint8_t **result);
+void runHollantiQueryThread(server *s, uint8_t **keys, int threadNum, int startIndex, int endIndex,
+                            uint8_t **result);
+void assembleHollantiQueryThreadResults(server *s, uint8_t ***in, int numThreads, uint8_t **out);
+
+/* ---- the other PIR modes' server entry points, bound by src/server_util/*.go
+ *      (shamir.go:52, multiparty.go:64, cd732.go:64, woodruff.go:69).  Their modes are outside
+ *      this engine's scope: setSystemParams refuses modes 1, 2, 4, 5, 6, and these abort with a
+ *      message if reached anyway.  The assemble functions are the reference's XOR folds
+ *      (server.cpp:304-319, 432-441, 494-503, 647-665). ---- */
+void runOptShamirDPFQueryThread(server *s, uint8_t **keys, int threadNum, int startIndex,
+                                int endIndex, uint8_t **result);
+void runOptimizedMultiPartyDPFQueryThread(server *s, uint8_t *key, int threadNum, int numThreads,
+                                          uint8_t **result);
+void runCDQueryThread(server *s, uint8_t *key, int threadNum, int numThreads, uint8_t **result);
+void runWoodruffQueryThread(server *s, uint8_t *key, int threadNum, int startIndex, int endIndex,
+                            uint8_t **result);
+void assembleShamirQueryThreadResults(server *s, uint8_t ***in, int numThreads, uint8_t **out);
+void assembleMultipartyDPFQueryThreadResults(server *s, uint8_t ***in, int numThreads,
+                                             uint8_t **out);
+void assembleCDQueryThreadResults(server *s, uint8_t ***in, int numThreads, uint8_t **out);
+void assembleWoodruffQueryThreadResults(server *s, uint8_t ***in, int numThreads, uint8_t **out);
+/* utils.h:29-30 */
+int calcShamirDPFKeyLength(int log_domainSize);
+int calcShamirResponseLength(int log_domainSize, int fileSizeBytes);
+
 void initialize_client(client *c, uint8_t log_num_files, uint32_t file_size_bytes);
 void free_client(client *c);
 void encode_across_files_server(client *c, server *s);
+/* client.cpp:93-110 (ENCODE_ACROSS == 0 modes, i.e. Hollanti): row i of party q =
+ * XOR_{j<K} gf_pow(q, j) * file_i[j*EFS .. (j+1)*EFS) (gen_encode_matrix, coding.cpp:64-70) */
+void encode_within_files_server(client *c, server *s);
 /* client-side erasure decode of one tree-mode query (client.h:33, client.cpp:211-268,
  * semi-honest: B == 0): responses[j][round][byte] from the NUM_PARTIES - R servers q with
  * erasureIndexList[q-1] == 1, in increasing q; output = the FILE_SIZE_BYTES record. */
 void assembleDPFTreeQueryResponses(client *c, uint8_t *erasureIndexList, uint8_t ***responses,
                                    uint8_t *output);
+/* client-side decode of one polynomial (Hollanti) query (client.h:46, client.cpp:499-552,
+ * semi-honest): responses[j][round][byte] from the NUM_PARTIES - R servers not erased */
+void assembleHollantiResponses(client *c, uint8_t *erasureIndexList, uint8_t ***responses,
+                               uint8_t *output);
 /* interpolation.h:10, interpolation.cpp:176-196 */
 void lagrangeInterpolationSemihonest(uint8_t *evalPoints, uint8_t numPoints, uint8_t *evals,
                                      uint8_t funcDegree, uint8_t *output);

@@ -275,4 +275,86 @@ int ref_e2e(int L, int f, int k, int r, int rho, int idx, uint8_t* files, uint8_
     return ok;
 }
 
+// Polynomial (Hollanti) PIR end to end, the harness of correctness_tests.cpp:924-1020 with the
+// Go server's setup (server.go:299-319, ENCODE_ACROSS == 0): setSystemParams(mode 3), the
+// synthetic DB, p servers encoded within files (client.cpp:99-103), generateHollantiQuery
+// (client.cpp:201-203 -> shamir_dpf.cpp:190-237), every party's runHollantiQuery answer, the
+// same answer from T runHollantiQueryThread slices + assembleHollantiQueryThreadResults
+// (server.cpp:345-382), the first r parties erased, assembleHollantiResponses (client.cpp:499).
+// Buffers: shards[p*N*efs], keys[p*nq*N], answers[p*nq*efs], thread_answers[p*nq*efs],
+// decoded[f].  Returns 1 when decoded == file[idx].
+int ref_hollanti_e2e(int L, int f, int t, int k, int r, int rho, int idx, int nthreads,
+                     uint8_t* shards, uint8_t* keys_out, uint8_t* answers,
+                     uint8_t* thread_answers, uint8_t* decoded) {
+    setSystemParams(L, f, t, k, r, 0, rho, 0, 3);
+    int p = NUM_PARTIES, nq = NUM_ROUNDS, efs = ENCODED_FILE_SIZE_BYTES;
+    size_t N = NUM_ENCODED_FILES;
+    client c;
+    initialize_client(&c, L, FILE_SIZE_BYTES);
+    std::vector<server> servers(p);
+    for (int i = 0; i < p; i++) {
+        initializeServer(&servers[i], i + 1, LOG_NUM_ENCODED_FILES, efs, 0, nthreads);
+        encode_within_files_server(&c, &servers[i]);
+        for (size_t j = 0; j < N; j++)
+            memcpy(shards + ((size_t)i * N + j) * efs, servers[i].indexList[j], efs);
+    }
+    uint8_t*** keys = (uint8_t***)malloc(p * sizeof(uint8_t**));
+    for (int i = 0; i < p; i++) {
+        keys[i] = (uint8_t**)malloc(nq * sizeof(uint8_t*));
+        for (int j = 0; j < nq; j++) keys[i][j] = (uint8_t*)malloc(NUM_FILES);
+    }
+    generateHollantiQuery(&c, idx, keys);
+    std::vector<std::vector<uint8_t*>> resp(p, std::vector<uint8_t*>(nq));
+    int slice = (int)N / nthreads;
+    for (int i = 0; i < p; i++) {
+        for (int j = 0; j < nq; j++) {
+            memcpy(keys_out + ((size_t)i * nq + j) * N, keys[i][j], N);
+            resp[i][j] = answers + ((size_t)i * nq + j) * efs;
+        }
+        runHollantiQuery(&servers[i], keys[i], resp[i].data());
+        uint8_t*** in = (uint8_t***)malloc(nthreads * sizeof(uint8_t**));
+        for (int th = 0; th < nthreads; th++) {
+            in[th] = (uint8_t**)malloc(nq * sizeof(uint8_t*));
+            for (int j = 0; j < nq; j++) in[th][j] = (uint8_t*)malloc(efs);
+            runHollantiQueryThread(&servers[i], keys[i], th, th * slice, (th + 1) * slice, in[th]);
+        }
+        std::vector<uint8_t*> out(nq);
+        for (int j = 0; j < nq; j++) out[j] = thread_answers + ((size_t)i * nq + j) * efs;
+        assembleHollantiQueryThreadResults(&servers[i], in, nthreads, out.data());
+        for (int th = 0; th < nthreads; th++) {
+            for (int j = 0; j < nq; j++) free(in[th][j]);
+            free(in[th]);
+        }
+        free(in);
+    }
+    std::vector<uint8_t> erasure(p);
+    for (int i = 0; i < p; i++) erasure[i] = (i < r) ? 0 : 1;
+    int numResponses = p - r;
+    uint8_t*** test = (uint8_t***)malloc(numResponses * sizeof(uint8_t**));
+    for (int i = 0, cur = 0; i < p; i++)
+        if (erasure[i]) test[cur++] = resp[i].data();
+    std::vector<uint8_t> out(FILE_SIZE_BYTES);
+    assembleHollantiResponses(&c, erasure.data(), test, out.data());
+    memcpy(decoded, out.data(), f);
+    int ok = memcmp(out.data(), c.unencoded_files[idx], f) == 0;
+    free(test);
+    for (int i = 0; i < p; i++) {
+        for (int j = 0; j < nq; j++) free(keys[i][j]);
+        free(keys[i]);
+    }
+    free(keys);
+    for (int i = 0; i < p; i++) freeServer(&servers[i]);
+    return ok;
+}
+
+// setSystemParams(L,f,t,k,r,0,rho,0,3) sizing: p, efs, nq
+void ref_hollanti_sizes(int L, int f, int t, int k, int r, int rho, int* out3) {
+    setSystemParams(L, f, t, k, r, 0, rho, 0, 3);
+    out3[0] = NUM_PARTIES;
+    out3[1] = ENCODED_FILE_SIZE_BYTES;
+    out3[2] = NUM_ROUNDS;
+}
+
+int ref_shamir_key_len(int n) { return calcShamirDPFKeyLength(n); }
+
 }  // extern "C"

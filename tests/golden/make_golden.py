@@ -210,15 +210,50 @@ def fullsize():
     write("fullsize.json", {"shard_seed": SHARD_SEED, "cases": cases})
 
 
+def hollanti():
+    """Polynomial (Hollanti) PIR, mode 3: keys from generateHollantiQuery, encode-within shards,
+    every party's runHollantiQuery answer and its T-thread assembled form, the decode."""
+    REF.ref_hollanti_e2e.restype = ctypes.c_int
+    cases = []
+    for (L, f, t, k, r, rho, idx, T) in [(10, 64, 1, 2, 1, 1, 77, 4), (12, 100, 2, 3, 2, 1, 1234, 8),
+                                         (11, 48, 1, 4, 1, 1, 5, 2), (9, 33, 1, 1, 0, 1, 511, 1)]:
+        s = (ctypes.c_int * 3)()
+        REF.ref_hollanti_sizes(L, f, t, k, r, rho, s)
+        p, efs, nq = list(s)
+        N = 1 << L
+        shards = np.zeros(p * N * efs, np.uint8)
+        keys = np.zeros(p * nq * N, np.uint8)
+        ans = np.zeros(p * nq * efs, np.uint8)
+        thr = np.zeros(p * nq * efs, np.uint8)
+        dec = np.zeros(f, np.uint8)
+        ok = REF.ref_hollanti_e2e(L, f, t, k, r, rho, idx, T, ptr(shards), ptr(keys), ptr(ans),
+                                  ptr(thr), ptr(dec))
+        assert ok == 1, (L, f, t, k, r, rho)
+        assert np.array_equal(ans, thr)
+        cases.append({
+            "L": L, "f": f, "t": t, "k": k, "r": r, "rho": rho, "index": idx, "threads": T,
+            "p": p, "efs": efs, "nq": nq,
+            "shard_sha256": [sha(shards[i * N * efs:(i + 1) * N * efs]) for i in range(p)],
+            "keys": [keys[i * nq * N:(i + 1) * nq * N].tobytes().hex() for i in range(p)],
+            "answers": [ans[i * nq * efs:(i + 1) * nq * efs].tobytes().hex() for i in range(p)],
+            "erasure": [0 if i < r else 1 for i in range(p)],
+            "decoded": dec.tobytes().hex(),
+        })
+        print("hollanti case", L, f, t, k, r, rho, "p", p, "nq", nq, "efs", efs)
+    write("hollanti.json", {"cases": cases,
+                            "shamir_key_len": {str(n): REF.ref_shamir_key_len(n) for n in (1, 2, 7, 10, 20, 25)}})
+
+
 if __name__ == "__main__":
     REF.ref_server_new.restype = ctypes.c_void_p
     REF.ref_blen.restype = ctypes.c_uint32
     for fn in (REF.ref_gf_mul, REF.ref_gf_pow, REF.ref_gf_inv):
         fn.restype = ctypes.c_uint8
-    what = sys.argv[1:] or ["prg", "gf", "dpf", "e2e", "thread", "fullsize"]
+    what = sys.argv[1:] or ["prg", "gf", "dpf", "e2e", "thread", "fullsize", "hollanti"]
     if "prg" in what: prg_kats()
     if "gf" in what: gf_kats()
     if "dpf" in what: dpf_and_answers()
     if "e2e" in what: e2e()
     if "thread" in what: thread_defect()
     if "fullsize" in what: fullsize()
+    if "hollanti" in what: hollanti()

@@ -39,6 +39,69 @@ def test_library_loads_and_exports_every_declared_symbol():
     assert names == set(_lib.PROTOTYPES)
 
 
+def declared_globals_and_types():
+    src = "".join(open(os.path.join(INCLUDE, h)).read() for h in sorted(os.listdir(INCLUDE))
+                  if h.endswith(".h"))
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    glob = set(re.findall(r"^extern\s+[\w\s\*]+?\b([A-Za-z_]\w*)\s*;", src, re.M))
+    types = set(re.findall(r"}\s*([A-Za-z_]\w*)\s*;", src))
+    return glob, types
+
+
+def test_header_declares_every_go_bound_name():
+    """Every name the reference's Go server side binds from package c (src/server/*.go,
+    src/server_util/*.go; inventory tests/golden/go_c_names.json from tools/go_c_names.py) is
+    declared by include/pir_server.h and exported by the library: SWIG over the drop-in header
+    generates the same Go names, so package server_util compiles against it unchanged."""
+    inv = O.golden("go_c_names.json")["names"]
+    funcs = declared_functions()
+    glob, types = declared_globals_and_types()
+    lib = _lib.load()
+    missing = []
+    for ent in inv:
+        kind, c = ent["kind"], ent["c"]
+        if kind == "function":
+            ok = c in funcs and hasattr(lib, c)
+        elif kind == "global":
+            ok = c in glob and hasattr(lib, c)
+        else:  # a struct type, its SWIG constructor / destructor
+            ok = c in types
+        if not ok:
+            missing.append((ent["go"], c, ent["sites"][0]))
+    assert len(inv) >= 30
+    assert not missing, missing
+
+
+def test_out_of_scope_modes_refuse_loudly():
+    """Modes the engine does not serve abort with a message (like the reference's
+    handleErrors), in a child process."""
+    import subprocess
+    import sys
+    code = ("from erasurecodedpir_amd import server as S; "
+            "S.setSystemParams(10, 64, 2, 2, 0, 0, 1, 0, 2)")
+    r = subprocess.run([sys.executable, "-c", code], cwd=O.ROOT, capture_output=True, text=True)
+    assert r.returncode != 0 and "outside the engine's scope" in r.stderr
+
+
+def test_hollanti_sizing_matches_reference():
+    from erasurecodedpir_amd import server
+    for case in O.golden("hollanti.json")["cases"]:
+        server.setSystemParams(case["L"], case["f"], case["t"], case["k"], case["r"], 0,
+                               case["rho"], 0, 3)
+        prm = server.params()
+        assert (prm["NUM_PARTIES"], prm["ENCODED_FILE_SIZE_BYTES"], prm["NUM_ROUNDS"],
+                prm["NUM_ENCODED_FILES"], prm["ENCODE_ACROSS"]) == \
+            (case["p"], case["efs"], case["nq"], 1 << case["L"], 0)
+
+
+def test_shamir_lengths_match_reference():
+    from erasurecodedpir_amd import _lib as L
+    lib = L.load()
+    for n, want in O.golden("hollanti.json")["shamir_key_len"].items():
+        assert lib.calcShamirDPFKeyLength(int(n)) == want
+        assert lib.calcShamirResponseLength(int(n), 100) == (want + 2) * 100
+
+
 def test_globals_exported():
     for g in _lib.GLOBALS_INT + _lib.GLOBALS_U32:
         _lib.global_int(g)
