@@ -117,6 +117,12 @@ struct pir_engine {
   uint8_t* d_result = nullptr;  // nq*efs (host-API staging)
   uint8_t* d_qscratch = nullptr;  // k_query super-tile tile inputs
   size_t qscratch_cap = 0;
+  uint32_t* d_qcnt = nullptr;     // k_query fused reduce: per-query slab counters (kept zero)
+  int qcnt_cap = 0;
+  // $PIR_FUSED_REDUCE=1: k_query's last workgroup XORs the slabs (no k_reduce launch).  Off by
+  // default: measured slower for a lone 2^20 x 1 KiB query (kernel 0.250 vs 0.218 ms; one
+  // workgroup's 256 KiB of cross-XCD sc1 loads outlast a k_reduce launch)
+  bool fused_reduce = false;
   uint8_t* d_coef_stage = nullptr;  // explicit-coefficient answers: host vectors staged here
   size_t coef_stage_cap = 0;
   uint8_t* h_key = nullptr;     // pinned
@@ -243,6 +249,21 @@ int answer_fused(pir_engine* e, const uint8_t* d_raw, int log_parts_total, uint6
   return PIR_OK;
 }
 
+// nk zeroed slab counters for k_query's fused reduce (the kernel leaves them zero)
+int ensure_qcnt(pir_engine* e, int nk, hipStream_t s) {
+  if (nk <= e->qcnt_cap) return PIR_OK;
+  if (e->d_qcnt) {
+    HIP_TRY(hipStreamSynchronize(s));
+    (void)hipFree(e->d_qcnt);
+  }
+  e->d_qcnt = nullptr;
+  e->qcnt_cap = 0;
+  HIP_TRY(hipMalloc(&e->d_qcnt, (size_t)nk * sizeof(uint32_t)));
+  HIP_TRY(hipMemsetAsync(e->d_qcnt, 0, (size_t)nk * sizeof(uint32_t), s));
+  e->qcnt_cap = nk;
+  return PIR_OK;
+}
+
 // one launch: key parse, tree and scan of nk queued keys (key_len apart) in k_query; then the
 // slab reduce of all nk answers (d_out: nk x nq x efs)
 int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, int nk,
@@ -252,6 +273,7 @@ int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, 
   const pir::ScanShape& sh = qp.shape;
   int rc = ensure_slabs(e, (size_t)nk * pir::query_slab_bytes(qp));
   if (!rc) rc = ensure_buf(&e->d_qscratch, &e->qscratch_cap, pir::query_scratch_bytes(qp));
+  if (!rc && e->fused_reduce) rc = ensure_qcnt(e, nk, s);
   if (rc) return rc;
   e->last_chunks = 1;
   e->last_fused = 2;
@@ -265,12 +287,13 @@ int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, 
   }
   HIP_TRY(pir::launch_query(qp, d_raw, (uint32_t)e->key_len, nk, c.num_parties,
                             c.log_num_records, c.party_index - 1, log_parts_total, prefix,
-                            e->d_shard + row0 * e->pitch, e->d_slabs, e->d_qscratch, s));
+                            e->d_shard + row0 * e->pitch, e->d_slabs, e->d_qscratch, s, nullptr,
+                            e->fused_reduce ? d_out : nullptr, e->d_qcnt, c.record_bytes));
   if (ev) {
     HIP_TRY(hipEventRecord(ev[EV_SCAN_E], s));
     HIP_TRY(hipEventRecord(ev[EV_PRERED], s));
   }
-  HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, d_out, s, nk));
+  if (!e->fused_reduce) HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, d_out, s, nk));
   if (ev) HIP_TRY(hipEventRecord(ev[EV_RED], s));
   return PIR_OK;
 }
@@ -674,6 +697,8 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
     e->allow_fused = !(f && f[0] == '0');
     const char* qy = getenv("PIR_QUERY");
     e->allow_query = !(qy && qy[0] == '0');
+    const char* fr = getenv("PIR_FUSED_REDUCE");
+    e->fused_reduce = fr && fr[0] == '1';
     const char* bg = getenv("PIR_BATCH_G");
     if (bg) e->batch_group = atoi(bg);
     const char* bb = getenv("PIR_BATCH_SCAN_BPC");
@@ -714,6 +739,7 @@ void pir_engine_destroy(pir_engine_t* e) {
                   (void*)e->nodes.t[1], (void*)e->d_c, (void*)e->d_slabs, (void*)e->d_part,
                   (void*)e->d_gather, (void*)e->d_result, (void*)e->d_cb, (void*)e->d_gtmp,
                   (void*)e->d_bpart, (void*)e->d_bgather, (void*)e->d_qscratch, (void*)e->d_coef_stage,
+                  (void*)e->d_qcnt,
                   (void*)e->bnodes.s[0],
                   (void*)e->bnodes.s[1], (void*)e->bnodes.t[0], (void*)e->bnodes.t[1]})
     if (p) (void)hipFree(p);
@@ -884,6 +910,7 @@ int pir_engine_reserve_queue(pir_engine_t* e, int num_keys) {
   if (!qp.tile) return PIR_OK;  // shapes k_query does not take allocate per answer
   int rc = ensure_slabs(e, (size_t)num_keys * pir::query_slab_bytes(qp));
   if (!rc) rc = ensure_buf(&e->d_qscratch, &e->qscratch_cap, pir::query_scratch_bytes(qp));
+  if (!rc && e->fused_reduce) rc = ensure_qcnt(e, num_keys, e->stream);
   if (!rc && e->comm) {
     const size_t total = (size_t)num_keys * c.num_rounds * c.record_bytes;
     rc = ensure_buf(&e->d_bpart, &e->bpart_cap, total);

@@ -123,10 +123,13 @@ inline size_t query_slab_bytes(const QueryPlan& qp) {
 constexpr int kQueryTraceSlots = 192;  // trace: per-workgroup phase stamps (wall clock, 100 MHz)
 // device scratch for the super-tile tile inputs (0 when ls == 0)
 size_t query_scratch_bytes(const QueryPlan& qp);
+// out != nullptr: the answers are reduced in-kernel (no launch_reduce): query k's nq x efs bytes
+// at out + k * nq * efs; qcnt = nk zeroed counters (the kernel leaves them zero)
 hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
                         int p, int n, int party0, int log_parts, uint64_t prefix,
                         const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
-                        uint64_t* trace = nullptr);
+                        uint64_t* trace = nullptr, uint8_t* out = nullptr,
+                        uint32_t* qcnt = nullptr, uint32_t efs = 0);
 // XOR the slabs, compact pitch -> record_bytes: d_out[a*efs + b]; nk queries (slabs of query k
 // grid.x*grid.y*slab_bytes apart, answers nq*efs bytes apart)
 hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t efs,

@@ -940,7 +940,7 @@ struct QuerySmem {
   uint4 lastcw[kMaxCW];
   uint4 stk_s[kMaxLevels + 1];      // right siblings on the current root-to-tile path
   uint32_t stk_t[kMaxLevels + 1];
-  uint32_t bar, sbar, ready;
+  uint32_t bar, sbar, ready, lastq;
   uint32_t consumed[RING];
 };
 
@@ -980,7 +980,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
     int party0, int log_parts, uint64_t prefix, int lr, int lt, int ls,
     uint4* __restrict__ fr_s, uint32_t* __restrict__ fr_t, const uint8_t* __restrict__ shard,
     uint32_t pitch, uint32_t cpr, uint32_t gy, uint8_t* __restrict__ slabs,
-    uint64_t* __restrict__ trace) {
+    uint64_t* __restrict__ trace, uint8_t* __restrict__ out, uint32_t* __restrict__ qcnt,
+    uint32_t efs) {
+  // out != nullptr: the slabs of each query are reduced in-kernel into out (query k at
+  // out + k * nq * efs; qcnt[k] zero on entry, left zero); else the host launches k_reduce.
   // trace != nullptr: per-workgroup wall-clock stamps (100 MHz) of query 0's phases,
   // kQueryTraceSlots apart (layout: pir_engine_trace_query, include/pir_engine.h)
   // diagnostics only: trace[kQueryTraceSlots * gridDim.x] bit 0 = scan waves skip their rows
@@ -991,7 +994,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
   constexpr int SW = kFusedWaves - TW;
   constexpr int CH = VEC * 4;
   constexpr int GW = kColGroupLanes * VEC;
-  constexpr int KT = TILE == 4096 ? 12 : 10;  // log2 TILE
+  constexpr int KT = TILE == 4096 ? 12 : (TILE == 1024 ? 10 : (TILE == 512 ? 9 : 8));  // log2 TILE
+  static_assert((1 << KT) == TILE, "TILE: 256, 512, 1024 or 4096 leaves");
   using Smem = QuerySmem<TILE, NRP, NQ, VEC, GYMAX, RING>;
   static_assert(sizeof(Smem) <= 160 * 1024, "LDS");
   __shared__ Smem sm;
@@ -1464,8 +1468,51 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
         for (uint32_t gg = 0; gg < gy; ++gg) {
           uint32_t* slab = qslab + ((uint64_t)gg * gridDim.x + blockIdx.x) * slab_words;
           for (int k = st; k < (int)slab_words; k += SW * 64) {
-            slab[k] = sm.red[gg][k];
+            if (out)  // read back by another workgroup below: stored past this XCD's L2 (sc1)
+              __hip_atomic_store(&slab[k], sm.red[gg][k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+              slab[k] = sm.red[gg][k];
             sm.red[gg][k] = 0;
+          }
+        }
+        if (out) {
+          // Fused reduce (no k_reduce launch): every scan wave's sc1 slab stores complete
+          // (vmcnt(0)) before the workgroup's ONE agent-scope counter add; the workgroup whose
+          // add comes last XORs the slabs of every workgroup with sc1 loads (the hand-off of
+          // MI355X_MICROARCH.md's first sc1 row: no L2 write-back or invalidate needed).
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          group_barrier(&sm.sbar, sgen, SW);
+          if (st == 0)
+            sm.lastq = __hip_atomic_fetch_add(qcnt + qy, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+          group_barrier(&sm.sbar, sgen, SW);
+          if (lds_load(&sm.lastq)) {
+            const uint32_t words = pitch / 4, P = (uint32_t)NQ * words, nth = SW * 64;
+            const uint32_t S = P >= nth ? 1u : nth / P;  // threads per output word
+            const uint32_t gx = gridDim.x;
+            for (uint32_t idx = (uint32_t)st; idx < P * S; idx += nth) {
+              const uint32_t pw = idx % P, part = idx / P;
+              const uint32_t a = pw / words, w = pw - a * words;
+              const uint32_t grp = w / GW, win = w - grp * GW;
+              const uint32_t* src = qslab + (uint64_t)grp * gx * slab_words + a * GW + win;
+              uint32_t acc = 0;
+              for (uint32_t x = part; x < gx; x += S)
+                acc ^= __hip_atomic_load(src + (uint64_t)x * slab_words, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+              if (acc) atomicXor(&sm.red[grp][a * GW + win], acc);
+            }
+            group_barrier(&sm.sbar, sgen, SW);
+            uint8_t* qout = out + (size_t)qy * NQ * efs;
+            for (uint32_t pw = (uint32_t)st; pw < P; pw += nth) {  // pitch -> record bytes
+              const uint32_t a = pw / words, w = pw - a * words;
+              const uint32_t grp = w / GW, win = w - grp * GW;
+              const uint32_t v = sm.red[grp][a * GW + win];
+              sm.red[grp][a * GW + win] = 0;
+              for (uint32_t t = 0; t < 4; ++t)
+                if (4 * w + t < efs) qout[(size_t)a * efs + 4 * w + t] = (uint8_t)(v >> (8 * t));
+            }
+            if (st == 0)  // ready for the next launch that answers a query in this slot
+              __hip_atomic_store(qcnt + qy, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         }
         group_barrier(&sm.sbar, sgen, SW);  // red[] is clear for the next query
@@ -1692,6 +1739,7 @@ TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last) {
 // ---- fused leaf stage + scan -----------------------------------------------------------------
 constexpr int kFusedTW = 8;       // tree waves per workgroup (the other 8 scan)
 constexpr int kQueryTreeHeavyTW = 12;  // k_query for small records: 12 tree + 4 scan waves
+constexpr int kLoneTile = 1024;        // leaves per tile of a lone query (nk == 1) of large records
 constexpr int kFusedTileIn = 64;  // tree nodes entering a tile
 
 int fused_tile(int nq, uint32_t pitch, uint64_t nleaves, int num_cus) {
@@ -1780,6 +1828,13 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
   // tile is built during the scan of the previous one, and wide tiles spend a smaller share of
   // their tree in latency-bound narrow levels (a lone query keeps 1024: shorter first tile)
   if (nk > 1 && nq <= 2 && nleaves >= (uint64_t)4096 * 256) tile = 4096;
+  // a lone query of large records waits for its first tile before any row is scanned: smaller
+  // tiles (fewer, cheaper levels under a deeper root) start the scan sooner ($PIR_QUERY_TILE1)
+  if (nk == 1 && nq <= 2 && pitch > 256 && tile == 1024) {
+    int t1 = kLoneTile;
+    if (const char* tv = getenv("PIR_QUERY_TILE1")) t1 = atoi(tv);
+    if (t1 == 256 || t1 == 512 || t1 == 1024) tile = t1;
+  }
   // records of <= 256 B: a tile's rows stream in a quarter of the time its tree takes, so 12 of
   // the 16 waves build trees and 4 scan ($PIR_QUERY_TW = 8 or 12 overrides)
   qp.tw = (nq <= 2 && pitch <= 256) ? kQueryTreeHeavyTW : kFusedTW;
@@ -1787,7 +1842,8 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
     const int v = atoi(tw);
     if (v == kFusedTW || (v == kQueryTreeHeavyTW && nq <= 2)) qp.tw = v;
   }
-  const int kt = tile == 4096 ? 12 : 10;
+  int kt = 0;
+  while ((1 << kt) < tile) ++kt;
   int lr = 0;
   while ((2ll << lr) <= num_cus) ++lr;  // regions = largest power of two <= CUs
   lr = std::min(lr, nr - kt);
@@ -1813,7 +1869,7 @@ template <int NQ, int TILE>
 static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
                            int p, int n, int party0, int log_parts, uint64_t prefix,
                            const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
-                           uint64_t* trace) {
+                           uint64_t* trace, uint8_t* out, uint32_t* qcnt, uint32_t efs) {
   uint4* fr_s = reinterpret_cast<uint4*>(scratch);
   uint32_t* fr_t = reinterpret_cast<uint32_t*>(scratch + ((size_t)qp.shape.grid.x << (kQueryKin + qp.ls)) * sizeof(uint4));
   constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : 8));
@@ -1824,7 +1880,7 @@ static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t k
   hipLaunchKernelGGL((k_query<NQ, NRP, VEC, UNI, TW, TILE, GY, RING>), dim3(sh.grid.x),          \
                      dim3(kFusedThreads), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,          \
                      log_parts, prefix, qp.lr, qp.lt, qp.ls, fr_s, fr_t, shard, sh.pitch, sh.cpr,  \
-                     gy, slabs, trace)
+                     gy, slabs, trace, out, qcnt, efs)
   if constexpr (NQ <= 2) {
     if (qp.tw == kQueryTreeHeavyTW) {  // small records: the tree is the bottleneck
       if (sh.uniform) PIR_QL(true, kQueryTreeHeavyTW, 4, sh.grid.y);
@@ -1845,18 +1901,21 @@ size_t query_scratch_bytes(const QueryPlan& qp) {
 hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
                         int p, int n, int party0, int log_parts, uint64_t prefix,
                         const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
-                        uint64_t* trace) {
-  if (nk < 1 || (qp.ls && !scratch)) return hipErrorInvalidValue;
-#define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, scratch, s, trace)
+                        uint64_t* trace, uint8_t* out, uint32_t* qcnt, uint32_t efs) {
+  if (nk < 1 || (qp.ls && !scratch) || (out && !qcnt)) return hipErrorInvalidValue;
+#define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, scratch, s, trace, out, qcnt, efs)
 #ifdef PIR_DEV_NQ  // development builds only (ISA / register checks): one round count
   return qp.shape.nq == PIR_DEV_NQ && qp.tile == 1024 ? PIR_Q(PIR_DEV_NQ, 1024) : hipErrorInvalidValue;
 #else
-  if (qp.tile == 4096) {
-    switch (qp.shape.nq) {
-      case 1: return PIR_Q(1, 4096);
-      case 2: return PIR_Q(2, 4096);
-      default: return hipErrorInvalidValue;
-    }
+  if (qp.tile == 4096 || qp.tile == 512 || qp.tile == 256) {
+    const int t = qp.tile, nq = qp.shape.nq;
+    if (t == 4096 && nq == 1) return PIR_Q(1, 4096);
+    if (t == 4096 && nq == 2) return PIR_Q(2, 4096);
+    if (t == 512 && nq == 1) return PIR_Q(1, 512);
+    if (t == 512 && nq == 2) return PIR_Q(2, 512);
+    if (t == 256 && nq == 1) return PIR_Q(1, 256);
+    if (t == 256 && nq == 2) return PIR_Q(2, 256);
+    return hipErrorInvalidValue;
   }
   if (qp.tile != 1024) return hipErrorInvalidValue;
   switch (qp.shape.nq) {

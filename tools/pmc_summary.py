@@ -1,13 +1,17 @@
 #!/usr/bin/env python3
-"""Summarise the rocprofv3 passes of tools/gpu_profile.sh into profiles/pmc_<cfg>.json.
+"""Summarise the rocprofv3 passes of tools/gpu_pmc.sh into profiles/pmc_<cfg>.json.
 
-    python tools/pmc_summary.py CFG QUERIES_PER_LAUNCH RECORDS RECORD_BYTES
+    python tools/pmc_summary.py CFG QUERIES_PER_LAUNCH RECORDS RECORD_BYTES [CLOCK_GHZ]
 
 Reads gpurun_out/prof_<cfg>/run_kernel_stats.csv (kernel trace + stats pass) and the
-counter_collection CSVs of the separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes
-(gpurun_out/pmcf_<cfg>, gpurun_out/pmcw_<cfg>).  The dominant kernel is the k_query instance
-with the largest total duration.  HBM read bytes = 2 x FETCH_SIZE x 1024 (gfx950: FETCH_SIZE
-counts half the bytes of 16-B-per-lane streaming reads, MI355X_MICROARCH.md §HBM)."""
+counter_collection CSVs of every separate --pmc pass gpurun_out/pmc_<cfg>_*/.  The dominant
+kernel is the k_query instance with the largest total duration; every counter is averaged over
+its launches.  HBM read bytes = 2 x FETCH_SIZE x 1024 (gfx950: FETCH_SIZE counts half the bytes
+of 16-B-per-lane streaming reads, MI355X_MICROARCH.md §HBM).
+
+Derived issue figures (per CU, over the kernel's GRBM_GUI_ACTIVE cycles): VALU instructions per
+SIMD per cycle against the SIMD's 0.5 (a wave64 VALU op occupies a SIMD-32 for 2 cycles), SALU
+and LDS instructions per CU per cycle; SQ_* cycle counters count quad-cycles on gfx950."""
 import csv
 import glob
 import json
@@ -15,6 +19,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CUS = 256
 
 
 def rows(pattern):
@@ -31,36 +36,47 @@ def main():
     dom = max((r for r in stats if "k_query" in r["Name"]), key=lambda r: float(r["TotalDurationNs"]))
     name = dom["Name"]
     avg_ns = float(dom["AverageNs"])
-
-    def counter(pass_dir, cname):
-        vals = {}
-        for r in rows(os.path.join(base, pass_dir, "**", "*counter_collection.csv")):
-            if r.get("Kernel_Name") == name and r.get("Counter_Name") == cname:
-                key = r.get("Dispatch_Id") or r.get("Correlation_Id")
-                vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
-        return sum(vals.values()) / len(vals) if vals else None, len(vals)
-
-    fetch_kb, nf = counter(f"pmcf_{cfg}", "FETCH_SIZE")
-    write_kb, nw = counter(f"pmcw_{cfg}", "WRITE_SIZE")
+    counters = {}
+    for d in sorted(glob.glob(os.path.join(base, f"pmc_{cfg}_*"))):
+        if not os.path.isdir(d):
+            continue
+        per = {}
+        for r in rows(os.path.join(d, "**", "*counter_collection.csv")):
+            if r.get("Kernel_Name") != name:
+                continue
+            key = (r["Counter_Name"], r.get("Dispatch_Id") or r.get("Correlation_Id"))
+            per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
+        for (cname, _), v in per.items():
+            counters.setdefault(cname, []).append(v)
+    avg = {k: sum(v) / len(v) for k, v in counters.items()}
+    nl = {k: len(v) for k, v in counters.items()}
     algo = nrec * efs * qpl
-    read_b = 2 * fetch_kb * 1024 if fetch_kb is not None else None
-    hbm = (read_b or 0) + (write_kb or 0) * 1024
-    out = {
-        "config": cfg,
-        "kernel": name.split("(")[0],
-        "queries_per_launch": qpl,
-        "launches_profiled": {"FETCH_SIZE": nf, "WRITE_SIZE": nw},
-        "FETCH_SIZE_KB_per_launch": fetch_kb,
-        "WRITE_SIZE_KB_per_launch": write_kb,
-        "correction": "gfx950 FETCH_SIZE reports 1/2 of wide coalesced streaming reads "
-                      "(MI355X_MICROARCH.md HBM): read bytes = 2 x FETCH_SIZE x 1024",
-        "hbm_bytes_per_launch": int(hbm),
-        "hbm_bytes_per_query": int(hbm / qpl),
-        "algorithmic_bytes_per_launch": algo,
-        "traffic_over_algorithmic": round(hbm / algo, 4),
-        "kernel_avg_ns_rocprof": avg_ns,
-        "achieved_GBps_rocprof": round(algo / avg_ns, 1),
-    }
+    out = {"config": cfg, "kernel": name.split("(")[0], "queries_per_launch": qpl,
+           "kernel_avg_ns_rocprof": avg_ns, "achieved_GBps_rocprof": round(algo / avg_ns, 1),
+           "algorithmic_bytes_per_launch": algo,
+           "counters_per_launch": {k: round(v, 1) for k, v in sorted(avg.items())},
+           "launches_per_counter": nl}
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        hbm = 2 * avg["FETCH_SIZE"] * 1024 + avg["WRITE_SIZE"] * 1024
+        out.update({
+            "correction": "gfx950 FETCH_SIZE reports 1/2 of wide coalesced streaming reads "
+                          "(MI355X_MICROARCH.md HBM): read bytes = 2 x FETCH_SIZE x 1024",
+            "hbm_bytes_per_launch": int(hbm), "hbm_bytes_per_query": int(hbm / qpl),
+            "traffic_over_algorithmic": round(hbm / algo, 4)})
+    gui = avg.get("GRBM_GUI_ACTIVE")
+    if gui:
+        d = {"gui_active_cycles": gui, "shader_clock_GHz_implied": round(gui / avg_ns, 3)}
+        if "SQ_INSTS_VALU" in avg:
+            d["valu_insts_per_simd_per_cycle"] = round(avg["SQ_INSTS_VALU"] / (CUS * 4) / gui, 4)
+            d["valu_issue_share_of_peak_0.5"] = round(avg["SQ_INSTS_VALU"] / (CUS * 4) / gui / 0.5, 4)
+        for k in ("SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD"):
+            if k in avg:
+                d[k.lower().replace("sq_insts_", "") + "_insts_per_cu_per_cycle"] = round(avg[k] / CUS / gui, 4)
+        if "SQ_INSTS_VALU" in avg:
+            d["valu_insts_per_shard_dword"] = round(avg["SQ_INSTS_VALU"] * 64 / (algo / 4), 3)
+        if "SQ_INSTS_SALU" in avg:
+            d["salu_insts_per_shard_dword"] = round(avg["SQ_INSTS_SALU"] * 64 / (algo / 4), 3)
+        out["issue"] = d
     dst = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
