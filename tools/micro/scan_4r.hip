@@ -82,6 +82,12 @@ __global__ __launch_bounds__(WAVES * 64) void k(const uint8_t* __restrict__ shar
                                                 const u32x8* __restrict__ mtab,
                                                 uint32_t* __restrict__ out) {
   constexpr int VEC = MODE == 6 ? 1 : 2;
+  __shared__ uint32_t lmt[256 * 8];  // MODE 7: the mask table in LDS
+  if constexpr (MODE == 7) {
+    for (int i = threadIdx.x; i < 256 * 8; i += blockDim.x)
+      lmt[i] = ((i >> 3) >> (i & 7)) & 1 ? 0xffffffffu : 0u;
+    __syncthreads();
+  }
   constexpr int GROUPS = 1024 / (64 * VEC * 4);  // column groups of a 1 KiB record
   constexpr int U = 8;
   const int lane = threadIdx.x & 63;
@@ -131,6 +137,22 @@ __global__ __launch_bounds__(WAVES * 64) void k(const uint8_t* __restrict__ shar
     if constexpr (MODE == 3) {
 #pragma unroll
       for (int u = 0; u < U; ++u) Z[0][0][0] ^= x[u][0];
+    } else if constexpr (MODE == 7) {
+      // masks from an LDS copy of the table: two broadcast ds_read_b128 per (row, round) into
+      // VGPRs -- no scalar instruction per plane or per round
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int a = 0; a < NQ; ++a) {
+          const uint32_t ca = ((a < 4 ? c0[u] : c1[u]) >> (8 * (a & 3))) & 0xffu;
+          const uint4* mp = reinterpret_cast<const uint4*>(lmt) + 2 * ca;
+          const uint4 m0 = mp[0], m1 = mp[1];
+          const uint32_t t[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+#pragma unroll
+          for (int b = 0; b < 8; ++b)
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) Z[a][b][v] = mxor(Z[a][b][v], x[u][v], t[b]);
+        }
     } else if constexpr (MODE == 2) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -235,7 +257,9 @@ int main() {
   run<3, 8>(shard, nrec, coef, mtab, out, cus);
   run<2, 8>(shard, nrec, coef, mtab, out, cus);
   run<6, 8>(shard, nrec, coef, mtab, out, cus);
+  run<7, 8>(shard, nrec, coef, mtab, out, cus);
   run<2, 16>(shard, nrec, coef, mtab, out, cus);
+  run<7, 16>(shard, nrec, coef, mtab, out, cus);
   run<6, 16>(shard, nrec, coef, mtab, out, cus);
   return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
