@@ -362,6 +362,38 @@ def roofline(kern_ms, local_bytes, K, config, world):
     }
 
 
+VALU_PEAK_SPEC_T = 256 * 128 * 2.4e9 / 1e12  # lane-ops/s: 256 CUs x 4 SIMD-32 x 2.4 GHz
+VALU_PEAK_MEASURED_T = 47.0  # 2-VGPR-source bitwise ops, all CUs (profiles/r02_micro/valu_rate.log)
+
+
+def _valu_roofline(config, world, kern_ms, queries_per_launch, leaves_per_query):
+    """Integer-VALU ceiling of the dominant kernel (the AES tree's secondary
+    roofline): VALU lane-ops per launch from the committed rocprofv3 --pmc SQ_INSTS_VALU pass
+    (wave instructions x 64 lanes), over this run's measured kernel time."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    if world != 1 or not os.path.exists(path) or not kern_ms or kern_ms != kern_ms:
+        return None
+    try:
+        d = json.load(open(path))
+        c = d.get("counters_per_launch", {})
+        insts = c.get("SQ_INSTS_VALU")
+        if not insts:
+            return None
+        q_prof = d.get("queries_per_launch", queries_per_launch)
+        ops_q = insts * 64 / q_prof
+        lds_q = c.get("SQ_INSTS_LDS", 0) * 64 / q_prof
+        achieved = ops_q * queries_per_launch / (kern_ms / 1e3) / 1e12
+        return {"bound": "valu", "unit": "T lane-ops/s",
+                "lane_ops_per_query": int(ops_q), "lane_ops_per_leaf": round(ops_q / leaves_per_query, 1),
+                "lds_lane_ops_per_leaf": round(lds_q / leaves_per_query, 1),
+                "achieved": round(achieved, 2), "peak_spec": round(VALU_PEAK_SPEC_T, 1),
+                "peak_measured": VALU_PEAK_MEASURED_T,
+                "frac_of_measured": round(achieved / VALU_PEAK_MEASURED_T, 3),
+                "source": f"profiles/pmc_{config}.json (SQ_INSTS_VALU, SQ_INSTS_LDS per launch)"}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def _pmc_traffic(config, world, queries_per_launch):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc passes
     (profiles/pmc_<config>.json: bytes per query, measured), scaled to the launch's queries.
@@ -500,6 +532,7 @@ def main():
                     "in one launch, the tree of query k+1 built while query k streams",
         },
         "roofline": rl,
+        "roofline_valu": _valu_roofline(config, world, kern_ms, K, float(eng.num_rows)),
         "single_query": {
             "ms_per_query": r5(m["ms1"]),
             "value": round(shard_bytes / GIB / (m["ms1"] / 1e3), 3),
