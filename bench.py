@@ -260,6 +260,19 @@ class Ctx:
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
         self.world, self.rank, self.local = world, rank, local
+        self.rehearsal = False
+
+    def fold(self, arr):
+        """Rehearsal runs only: XOR of every rank's partition answer (gloo all-gather)."""
+        if not self.rehearsal:
+            return arr
+        t = self.torch.from_numpy(np.ascontiguousarray(arr))
+        parts = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t)
+        out = parts[0].numpy().copy()
+        for p in parts[1:]:
+            out ^= p.numpy()
+        return out
 
     def timed(self, eng, fn):
         self.sync(eng)
@@ -333,7 +346,7 @@ def pir_check(ctx, eng, keyset, fcw, q_answers, n, g):
     eng.set_party(2)
     ok = True
     for q, (idx, ks) in enumerate(keyset):
-        a2 = eng.answer(ks[1])
+        a2 = ctx.fold(eng.answer(ks[1]))
         owner = idx >> (n - g) if g else 0
         rec = eng.shard_row(idx - owner * eng.num_rows) if ctx.rank == owner else None
         if ctx.world > 1:
@@ -447,8 +460,15 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    # PIR_BENCH_REHEARSAL=1 (diagnostics, N > 1 on a box with fewer GPUs): ranks share the
+    # visible GPUs, no RCCL communicator is attached, and the partition answers are XOR-folded
+    # over gloo on the host for the parity checks (the timed region then holds no exchange)
+    rehearsal = world > 1 and os.environ.get("PIR_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     ctx = Ctx(world, rank, local)
+    ctx.rehearsal = rehearsal
 
     import erasurecodedpir_amd as pir
     from erasurecodedpir_amd.dist import broadcast_bytes, log2_exact
@@ -469,10 +489,12 @@ def main():
 
     eng = pir.Engine(p, 1, n, efs, nq, device=local, log_num_partitions=g, partition_index=rank)
     eng.fill_shard_random(SHARD_SEED)
-    if world > 1:
+    if world > 1 and not rehearsal:
         uid = broadcast_bytes(pir.comm_unique_id() if rank == 0 else None)
         eng.attach_comm(uid, world, rank)
     m = measure(ctx, eng, [ks[0] for _, ks in keyset], W, K, single=not args.queue_only)
+    if rehearsal and not args.queue_only:
+        m["answers"], m["singles"] = ctx.fold(m["answers"]), ctx.fold(m["singles"])
     ms = m["ms"]
     shard_bytes = float(1 << n) * efs  # logical shard (all ranks)
     value = shard_bytes / GIB / (ms / 1e3)
@@ -498,6 +520,7 @@ def main():
     t1 = time.perf_counter()
     for _ in range(incl_steps):
         a1 = eng.answer(k0)
+    a1 = ctx.fold(a1)
     incl_ms = (time.perf_counter() - t1) / incl_steps * 1e3
     same = bool(np.array_equal(a1, m["singles"][0]))
     queue_same = bool(np.array_equal(m["answers"], m["singles"]))
@@ -526,7 +549,9 @@ def main():
             f"split shard, weak scaling: {world} x 2^{n_cfg} x {efs} B partitions of one 2^{n} x {efs} B logical shard (RCCL all-gather + XOR fold)",
             "records": 1 << n, "record_bytes": efs, "parties": p, "num_rounds": nq,
             "records_per_gpu": int(eng.num_rows), "dpf_depth": n,
-            "parallelism": f"split-shard x{world}" if world > 1 else "single",
+            "parallelism": (f"split-shard x{world}" + (" (REHEARSAL: shared GPU, no RCCL, "
+                            "host gloo fold outside the timed region)" if rehearsal else ""))
+                           if world > 1 else "single",
             "step": "one PIR query: its own DPF key and tree, one full pass over the shard",
             "mode": "query queue: the K timed queries (distinct keys) are answered back to back "
                     "in one launch, the tree of query k+1 built while query k streams",
