@@ -76,6 +76,11 @@ PROTOTYPES = {
     "pir_engine_eval_all": (_I, [_P, _P, _P]),
     "pir_engine_answer_coefs": (_I, [_P, ctypes.POINTER(_P), _U64, _U64, _P]),
     "pir_engine_answer_coefs_dev": (_I, [_P, _P, _U64, _U64, _U64, _P, _P]),
+    "pir_engine_answer_mp": (_I, [_P, _P, _U64, _I, _I, _I, _I, _P]),
+    "pir_engine_answer_mp_dev": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
+    "pir_engine_mp_num_keys": (_I, [_I, _I]),
+    "pir_engine_mp_key_len": (_I, [_I, _I, _I]),
+    "pir_engine_mp_eval_bytes": (ctypes.c_longlong, [_I, _I, _I]),
     "pir_engine_answer_dev": (_I, [_P, _P, _P, _P]),
     "pir_engine_answer_batch_dev": (_I, [_P, _P, _I, _P, _P]),
     "pir_engine_answer_batch": (_I, [_P, _P, _I, _P]),
@@ -129,6 +134,8 @@ PROTOTYPES = {
     "encode_within_files_server": (None, [ctypes.POINTER(CClient), ctypes.POINTER(CServer)]),
     "runOptShamirDPFQueryThread": (None, [ctypes.POINTER(CServer), ctypes.POINTER(c_u8_p), _I, _I,
                                           _I, ctypes.POINTER(c_u8_p)]),
+    "calcMultiPartyOptDPFKeyLength": (_I, [_I, _I, _I]),
+    "runOptimizedMultiPartyDPFQuery": (None, [ctypes.POINTER(CServer), _P, ctypes.POINTER(c_u8_p)]),
     "runOptimizedMultiPartyDPFQueryThread": (None, [ctypes.POINTER(CServer), _P, _I, _I,
                                                     ctypes.POINTER(c_u8_p)]),
     "runCDQueryThread": (None, [ctypes.POINTER(CServer), _P, _I, _I, ctypes.POINTER(c_u8_p)]),

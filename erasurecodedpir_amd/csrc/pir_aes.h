@@ -112,15 +112,18 @@ __device__ __forceinline__ uint32_t last_col(const Tab& T, uint32_t a, uint32_t 
 
 constexpr uint32_t kRcon[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
 
-// Row shape, one key, NB CTR blocks with counters 0..NB-1; block NB-1 only needs its first
-// LASTW output words (the control-bit bytes); out[b] = AES_key(BE128(b)).
+// Row shape, one key, NB CTR blocks with counters c0..c0+NB-1 (c0 a multiple of NB, NB <= 256,
+// passed as ctr_be = the byte-swapped c0, i.e. BE128(c0)'s last word); block NB-1 only needs its
+// first LASTW output words (the control-bit bytes); out[b] = AES_key(BE128(c0 + b)).  The
+// counters differ in byte 15 only.
 template <int NB, int LASTW>
-__device__ __forceinline__ void aes_ctr_row(const Tab& T, uint4 key, uint4 (&out)[NB]) {
+__device__ __forceinline__ void aes_ctr_row(const Tab& T, uint4 key, uint4 (&out)[NB],
+                                            uint32_t ctr_be = 0) {
   uint32_t k0 = key.x, k1 = key.y, k2 = key.z, k3 = key.w;
   uint32_t w[NB][4];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    w[b][0] = k0; w[b][1] = k1; w[b][2] = k2; w[b][3] = k3 ^ ((uint32_t)b << 24);
+    w[b][0] = k0; w[b][1] = k1; w[b][2] = k2; w[b][3] = k3 ^ ctr_be ^ ((uint32_t)b << 24);
   }
 #pragma unroll
   for (int r = 0; r < 9; ++r) {

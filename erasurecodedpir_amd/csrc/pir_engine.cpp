@@ -21,6 +21,7 @@
 #include "../../include/pir_engine.h"
 #include "pir_coefs.h"
 #include "pir_kernels.h"
+#include "pir_mp.h"
 
 namespace {
 
@@ -125,6 +126,8 @@ struct pir_engine {
   bool fused_reduce = false;
   uint8_t* d_coef_stage = nullptr;  // explicit-coefficient answers: host vectors staged here
   size_t coef_stage_cap = 0;
+  uint8_t* d_mpkey = nullptr;       // multiparty DPF keys: host keys / unaligned device keys
+  size_t mpkey_cap = 0;
   uint8_t* h_key = nullptr;     // pinned
   uint8_t* h_res = nullptr;     // pinned
   std::vector<DevBuf> user;     // pir_engine_alloc_dev
@@ -625,6 +628,52 @@ int answer_coefs_locked(pir_engine* e, const uint8_t* src, uint64_t pitch, uint6
   return PIR_OK;
 }
 
+// Multiparty sqrt(N) DPF answer (server.cpp:384-430): the thread's rows of the domain
+// [thr * slice * mu, (thr + 1) * slice * mu), slice = nu / num_threads (the reference drops the
+// nu % num_threads remainder rows; so does this), intersected with this engine's partition:
+// shares (k_mp_shares) -> GF(2^8) scan -> slab reduce [-> all-gather + XOR fold].
+int answer_mp_locked(pir_engine* e, const pir::MpLayout& L, const uint8_t* d_key, int thread_num,
+                     int num_threads, uint8_t* d_result, hipStream_t s) {
+  const auto& c = e->cfg;
+  const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
+  uint8_t* out = e->comm ? e->d_part : d_result;
+  e->ev = nullptr;
+  const uint64_t slice = L.nu / (uint64_t)num_threads;
+  const uint64_t p0 = (uint64_t)c.partition_index * e->rows;
+  const uint64_t lo = std::max<uint64_t>((uint64_t)thread_num * slice * L.mu, p0);
+  const uint64_t hi = std::min<uint64_t>((uint64_t)(thread_num + 1) * slice * L.mu, p0 + e->rows);
+  if (hi <= lo) {
+    HIP_TRY(hipMemsetAsync(out, 0, out_bytes, s));
+  } else {
+    const uint64_t nrows = hi - lo;
+    const pir::ScanShape sh = pir::make_scan_shape(nrows, e->pitch, c.num_rounds, e->num_cus);
+    int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
+    if (rc) return rc;
+    HIP_TRY(pir::launch_mp_shares(L, d_key, lo, hi, e->nrp, e->d_c, e->num_cus, s));
+    HIP_TRY(pir::launch_scan(sh, e->d_shard + (lo - p0) * e->pitch, nrows, e->d_c, e->d_slabs,
+                             false, s));
+    HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, out, s));
+  }
+  if (e->comm) {
+    RCCL_TRY(ncclAllGather(e->d_part, e->d_gather, out_bytes, ncclUint8, e->comm, s));
+    HIP_TRY(pir::launch_xor_fold(e->d_gather, e->nranks, out_bytes, d_result, s));
+  }
+  return PIR_OK;
+}
+
+int check_mp(const pir_engine* e, int p, int t, int thread_num, int num_threads,
+             pir::MpLayout* L) {
+  if (!pir::mp_layout(p, e->cfg.log_num_records, t, L))
+    return fail(PIR_EINVAL, "no multiparty DPF layout for p=%d t=%d n=%d", p, t,
+                e->cfg.log_num_records);
+  if (L->nrk != e->cfg.num_rounds)
+    return fail(PIR_EINVAL, "p=%d t=%d gives %d shares (NUM_RSS_KEYS) but the engine has %d rounds",
+                p, t, L->nrk, e->cfg.num_rounds);
+  if (num_threads < 1 || thread_num < 0 || thread_num >= num_threads)
+    return fail(PIR_EINVAL, "thread_num %d of %d", thread_num, num_threads);
+  return PIR_OK;
+}
+
 int check_rows(const pir_engine* e, uint64_t row0, uint64_t nrows) {
   if (row0 > e->rows || nrows > e->rows - row0)
     return fail(PIR_EINVAL, "rows [%llu,%llu) beyond the %llu held", (unsigned long long)row0,
@@ -686,6 +735,7 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
         hipEventCreateWithFlags(&e->ev_cb_free[i], hipEventDisableTiming) != hipSuccess)
       return cleanup(fail(PIR_EHIP, "hipEventCreate failed"));
   pir::upload_aes_table(e->stream);
+  pir::upload_mp_aes_table(e->stream);
   const size_t shard_bytes = (size_t)e->rows * e->pitch;
   if (hipMalloc(&e->d_shard, shard_bytes) != hipSuccess)
     return cleanup(fail(PIR_ENOMEM, "hipMalloc shard %zu bytes", shard_bytes));
@@ -739,7 +789,7 @@ void pir_engine_destroy(pir_engine_t* e) {
                   (void*)e->nodes.t[1], (void*)e->d_c, (void*)e->d_slabs, (void*)e->d_part,
                   (void*)e->d_gather, (void*)e->d_result, (void*)e->d_cb, (void*)e->d_gtmp,
                   (void*)e->d_bpart, (void*)e->d_bgather, (void*)e->d_qscratch, (void*)e->d_coef_stage,
-                  (void*)e->d_qcnt,
+                  (void*)e->d_qcnt, (void*)e->d_mpkey,
                   (void*)e->bnodes.s[0],
                   (void*)e->bnodes.s[1], (void*)e->bnodes.t[0], (void*)e->bnodes.t[1]})
     if (p) (void)hipFree(p);
@@ -978,6 +1028,67 @@ int pir_engine_answer_coefs(pir_engine_t* e, const uint8_t* const* coefs, uint64
                            hipMemcpyHostToDevice, e->stream));
   rc = ws_release(e, e->stream, answer_coefs_locked(e, e->d_coef_stage, nrows, row0, nrows,
                                                     e->d_result, e->stream));
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(e->h_res, e->d_result, out_bytes, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memcpy(result, e->h_res, out_bytes);
+  return PIR_OK;
+}
+
+int pir_engine_mp_num_keys(int p, int t) {  // params.cpp:618
+  if (p < 1 || t < 0 || t > p) return 0;
+  return pir::mp_choose(p, t) * (p - t) / p;
+}
+
+int pir_engine_mp_key_len(int p, int n, int t) {  // utils.cpp:105-116 (its own mu = 2^(n/2))
+  if (p < 1 || t < 0 || t > p || n < 0 || n > 62) return 0;
+  const int c = pir::mp_choose(p, t), q = (p - t) * c / p;
+  if (c < 1 || c > 32) return 0;
+  const uint64_t p2 = 1ull << (c - 1), mu = 1ull << (n / 2), nu = 1ull << (n - n / 2);
+  return (int)(16 * p2 * nu + (uint64_t)q * nu * p2 + p2 * mu);
+}
+
+long long pir_engine_mp_eval_bytes(int p, int n, int t) {
+  pir::MpLayout L;
+  return pir::mp_layout(p, n, t, &L) ? (long long)L.eval_bytes : -1;
+}
+
+int pir_engine_answer_mp_dev(pir_engine_t* e, const uint8_t* d_key, int p, int t, int thread_num,
+                             int num_threads, uint8_t* d_result, void* stream) {
+  if (!e || !d_result) return fail(PIR_EINVAL, "null argument");
+  if (int rc = check_key_ptr(d_key)) return rc;
+  pir::MpLayout L;
+  if (int rc = check_mp(e, p, t, thread_num, num_threads, &L)) return rc;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  if (int rc = ws_acquire(e, s)) return rc;
+  if (((uintptr_t)d_key & 15) && L.eval_bytes) {  // the seeds are read as 16-byte words
+    if (int rc = ensure_buf(&e->d_mpkey, &e->mpkey_cap, L.eval_bytes)) return rc;
+    HIP_TRY(hipMemcpyAsync(e->d_mpkey, d_key, L.eval_bytes, hipMemcpyDeviceToDevice, s));
+    d_key = e->d_mpkey;
+  }
+  return ws_release(e, s, answer_mp_locked(e, L, d_key, thread_num, num_threads, d_result, s));
+}
+
+int pir_engine_answer_mp(pir_engine_t* e, const uint8_t* key, uint64_t key_bytes, int p, int t,
+                         int thread_num, int num_threads, uint8_t* result) {
+  if (!e || !result) return fail(PIR_EINVAL, "null argument");
+  if (int rc = check_key_ptr(key)) return rc;
+  pir::MpLayout L;
+  if (int rc = check_mp(e, p, t, thread_num, num_threads, &L)) return rc;
+  if (key_bytes < L.eval_bytes)
+    return fail(PIR_EINVAL, "multiparty key of %llu bytes; the evaluation reads %llu",
+                (unsigned long long)key_bytes, (unsigned long long)L.eval_bytes);
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const size_t out_bytes = (size_t)e->cfg.num_rounds * e->cfg.record_bytes;
+  if (int rc = ws_acquire(e, e->stream)) return rc;
+  if (int rc = ensure_buf(&e->d_mpkey, &e->mpkey_cap, std::max<uint64_t>(16, L.eval_bytes))) return rc;
+  if (L.eval_bytes)
+    HIP_TRY(hipMemcpyAsync(e->d_mpkey, key, L.eval_bytes, hipMemcpyHostToDevice, e->stream));
+  int rc = ws_release(e, e->stream, answer_mp_locked(e, L, e->d_mpkey, thread_num, num_threads,
+                                                     e->d_result, e->stream));
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(e->h_res, e->d_result, out_bytes, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));

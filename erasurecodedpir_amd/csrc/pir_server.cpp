@@ -38,7 +38,7 @@ int IS_HERMITE = 0;
 int D = 0;
 int MAC_SIZE_BYTES = 32;
 int CHECK_MAC = 0;
-int NUM_RSS_KEYS = 0;  // params.cpp:39-46 defaults; their modes are not served
+int NUM_RSS_KEYS = 0;  // params.cpp:39-46 defaults (CD / Woodruff modes are not served)
 int NUM_CD_KEYS = 0;
 int WOODRUFF_M = 0;
 int WOODRUFF_D = 0;
@@ -318,13 +318,18 @@ int calcOptimizedDPFTreeKeyLength(int p, int log_domainSize, int numQueries) {
   return pir_engine_key_len(p, log_domainSize, numQueries);
 }
 
-// params.cpp:467-512 with setModeParams(Tree) (params.cpp:414-418) or setModeParams(Hollanti)
-// (params.cpp:430-433); the other modes (multiparty, Shamir, CD, Woodruff, Goldberg) abort
+// params.cpp:372 isRss: cleared for good by the covering-design setups of params.cpp:520-599
+// (with the default M = 4 only the T = 2, p = 12 / 14 / 16 ones apply)
+static bool g_is_rss = true;
+
+// params.cpp:467-512 with setModeParams(Tree) (params.cpp:414-418), setModeParams(Multiparty)
+// (:419-422) or setModeParams(Hollanti) (:430-433), and the RSS share count of :603-619; the
+// other modes (Shamir, CD, Woodruff, Goldberg) abort
 void setSystemParams(int logNumFiles, int fileSizeBytes, int t, int k, int r, int b, int rho,
                      int checkMac, int mode) {
-  if (mode != 0 && mode != 3) {
-    fprintf(stderr, "pir shim: mode %d is outside the engine's scope (tree = 0, Hollanti = 3)\n",
-            mode);
+  if (mode != 0 && mode != 1 && mode != 3) {
+    fprintf(stderr, "pir shim: mode %d is outside the engine's scope (tree = 0, multiparty = 1, "
+            "Hollanti = 3)\n", mode);
     abort();
   }
   if (mode == 0 && t != 1) {  // params.cpp:415 assert(T == 1)
@@ -342,8 +347,8 @@ void setSystemParams(int logNumFiles, int fileSizeBytes, int t, int k, int r, in
   FILE_SIZE_BYTES = (uint32_t)fileSizeBytes;
   CHECK_MAC = checkMac;
   MODE = mode;
-  NUM_PARTIES = K + R + T + 2 * B + (RHO - 1);  // the same sum for both modes
-  ENCODE_ACROSS = mode == 0 ? 1 : 0;
+  NUM_PARTIES = K + R + T + 2 * B + (mode == 1 ? 0 : RHO - 1);
+  ENCODE_ACROSS = mode == 3 ? 0 : 1;
   NUM_RESPONSES = NUM_PARTIES - R;
   if (ENCODE_ACROSS) {
     LOG_NUM_ENCODED_FILES = ceil_log2((NUM_FILES + k - 1) / k);
@@ -361,6 +366,13 @@ void setSystemParams(int logNumFiles, int fileSizeBytes, int t, int k, int r, in
     ENCODED_FILE_SIZE_BYTES = (int)((FILE_SIZE_BYTES + k - 1) / k);
   }
   NUM_ROUNDS = (K == 1) ? 1 : K / RHO;
+  if (T == 2 && (NUM_PARTIES == 12 || NUM_PARTIES == 14 || NUM_PARTIES == 16)) g_is_rss = false;
+  if (t >= 1 && g_is_rss) NUM_RSS_KEYS = pir_engine_mp_num_keys(NUM_PARTIES, T);
+}
+
+// utils.cpp:105-116
+int calcMultiPartyOptDPFKeyLength(int p, int log_domainSize, int t) {
+  return pir_engine_mp_key_len(p, log_domainSize, t);
 }
 
 // utils.cpp:131-143
@@ -499,6 +511,41 @@ void assembleShamirQueryThreadResults(server* s, uint8_t*** in, int numThreads, 
            (size_t)calcShamirResponseLength(LOG_NUM_ENCODED_FILES, ENCODED_FILE_SIZE_BYTES));
 }
 
+// ---- multiparty sqrt(N) DPF PIR: the key's shares evaluated and scanned on the engine -------
+static void mp_answer(server* s, uint8_t* key, int threadNum, int numThreads, uint8_t** result,
+                      const char* fn) {
+  ShimState* st = state_of(s);
+  std::lock_guard<std::mutex> lk(st->mu);
+  pir_engine_t* e = engine_for(s, st, NUM_RSS_KEYS);
+  const size_t efs = (size_t)ENCODED_FILE_SIZE_BYTES;
+  std::vector<uint8_t> out((size_t)NUM_RSS_KEYS * efs);
+  const int kl = calcMultiPartyOptDPFKeyLength(NUM_PARTIES, LOG_NUM_ENCODED_FILES, T);
+  if (pir_engine_answer_mp(e, key, (uint64_t)(kl > 0 ? kl : 0), NUM_PARTIES, T, threadNum,
+                           numThreads, out.data()) != PIR_OK)
+    die(fn);
+  for (int a = 0; a < NUM_RSS_KEYS; ++a) memcpy(result[a], out.data() + a * efs, efs);
+}
+
+// server.cpp:136-176: random answers for a Byzantine server, else the whole domain
+void runOptimizedMultiPartyDPFQuery(server* s, uint8_t* key, uint8_t** result) {
+  state_of(s);
+  if (s->isByzantine) {  // gen_rand_bytes (server.cpp:157-160)
+    static std::mutex rmu;
+    static std::mt19937_64 rng{std::random_device{}()};
+    std::lock_guard<std::mutex> lk(rmu);
+    for (int a = 0; a < NUM_RSS_KEYS; ++a)
+      for (int j = 0; j < ENCODED_FILE_SIZE_BYTES; ++j) result[a][j] = (uint8_t)rng();
+    return;
+  }
+  mp_answer(s, key, 0, 1, result, "runOptimizedMultiPartyDPFQuery");
+}
+
+// server.cpp:384-430 (both branches compute the honest answer)
+void runOptimizedMultiPartyDPFQueryThread(server* s, uint8_t* key, int threadNum, int numThreads,
+                                          uint8_t** result) {
+  mp_answer(s, key, threadNum, numThreads, result, "runOptimizedMultiPartyDPFQueryThread");
+}
+
 void assembleMultipartyDPFQueryThreadResults(server* s, uint8_t*** in, int numThreads,
                                              uint8_t** out) {
   (void)s;  // server.cpp:432-441
@@ -518,9 +565,6 @@ void assembleWoodruffQueryThreadResults(server* s, uint8_t*** in, int numThreads
 
 void runOptShamirDPFQueryThread(server*, uint8_t**, int, int, int, uint8_t**) {
   out_of_scope("runOptShamirDPFQueryThread", "Shamir");
-}
-void runOptimizedMultiPartyDPFQueryThread(server*, uint8_t*, int, int, uint8_t**) {
-  out_of_scope("runOptimizedMultiPartyDPFQueryThread", "multiparty DPF");
 }
 void runCDQueryThread(server*, uint8_t*, int, int, uint8_t**) {
   out_of_scope("runCDQueryThread", "covering-design");

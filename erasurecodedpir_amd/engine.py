@@ -175,6 +175,24 @@ class Engine:
         check(self._lib.pir_engine_answer_coefs_dev(self._h, d_coefs, coef_pitch, row0, nrows,
                                                     d_result, stream), "answer_coefs_dev")
 
+    def answer_mp(self, key, p, t, thread_num=0, num_threads=1):
+        """Multiparty sqrt(N) DPF answer (runOptimizedMultiPartyDPFQuery[Thread], src/c/
+        server.cpp:136-176, :384-430): the key's NUM_RSS_KEYS shares of every record (the
+        layout of multiparty_dpf.cpp:467-539) scanned against the shard.  The engine's
+        num_rounds must be mp_num_keys(p, t).  -> (num_rounds, record_bytes)."""
+        k = np.frombuffer(bytes(key), np.uint8) if not isinstance(key, np.ndarray) else \
+            np.ascontiguousarray(key, np.uint8)
+        out = np.empty((self.num_rounds, self.record_bytes), np.uint8)
+        check(self._lib.pir_engine_answer_mp(self._h, k.ctypes.data_as(ctypes.c_void_p), k.size,
+                                             p, t, thread_num, num_threads,
+                                             out.ctypes.data_as(ctypes.c_void_p)),
+              "pir_engine_answer_mp")
+        return out
+
+    def answer_mp_dev(self, d_key, p, t, d_result, thread_num=0, num_threads=1, stream=None):
+        check(self._lib.pir_engine_answer_mp_dev(self._h, d_key, p, t, thread_num, num_threads,
+                                                 d_result, stream), "answer_mp_dev")
+
     def eval_all(self, key):
         """(num_rounds, rows) DPF shares dataShare[a][i]."""
         k, kp = self._check_key(key)
@@ -290,6 +308,21 @@ class Engine:
     def attach_comm(self, unique_id, nranks, rank):
         uid, up = _buf(unique_id)
         check(self._lib.pir_comm_attach(self._h, up, nranks, rank), "pir_comm_attach")
+
+
+def mp_num_keys(p, t):
+    """NUM_RSS_KEYS = choose(p, t) * (p - t) / p (params.cpp:618): shares per multiparty key."""
+    return _lib.load().pir_engine_mp_num_keys(p, t)
+
+
+def mp_key_len(p, n, t):
+    """calcMultiPartyOptDPFKeyLength (utils.cpp:105-116)."""
+    return _lib.load().pir_engine_mp_key_len(p, n, t)
+
+
+def mp_eval_bytes(p, n, t):
+    """Key bytes the multiparty evaluation reads (multiparty_dpf.cpp:485-511); -1: no layout."""
+    return _lib.load().pir_engine_mp_eval_bytes(p, n, t)
 
 
 def comm_unique_id():

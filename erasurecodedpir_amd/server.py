@@ -97,6 +97,26 @@ class Server:
             self._lib.runHollantiQueryThread(ctypes.byref(self.s), kp, *thread, _row_ptrs(out))
         return out
 
+    def runOptimizedMultiPartyDPFQuery(self, key):
+        """Multiparty sqrt(N) DPF answer (server.cpp:136-176): (NUM_RSS_KEYS, EFS)."""
+        return self._mp(key, None)
+
+    def runOptimizedMultiPartyDPFQueryThread(self, key, threadNum, numThreads):
+        """Rows of thread threadNum of numThreads (server.cpp:384-430)."""
+        return self._mp(key, (threadNum, numThreads))
+
+    def _mp(self, key, thread):
+        efs = _lib.global_int("ENCODED_FILE_SIZE_BYTES")
+        out = np.zeros((_lib.global_int("NUM_RSS_KEYS"), efs), np.uint8)
+        k = np.frombuffer(bytes(key), np.uint8).copy()
+        kp = k.ctypes.data_as(ctypes.c_void_p)
+        if thread is None:
+            self._lib.runOptimizedMultiPartyDPFQuery(ctypes.byref(self.s), kp, _row_ptrs(out))
+        else:
+            self._lib.runOptimizedMultiPartyDPFQueryThread(ctypes.byref(self.s), kp, *thread,
+                                                           _row_ptrs(out))
+        return out
+
     def freeServer(self):
         if self.s.ctx:
             self._lib.freeServer(ctypes.byref(self.s))
@@ -126,6 +146,16 @@ def assemblDPFTreeQueryThreadResults(server, parts):
 def assembleHollantiQueryThreadResults(server, parts):
     """parts: (numThreads, NUM_ROUNDS, EFS) -> (NUM_ROUNDS, EFS) (src/c/server.cpp:373-382)."""
     return _assemble("assembleHollantiQueryThreadResults", server, parts)
+
+
+def assembleMultipartyDPFQueryThreadResults(server, parts):
+    """parts: (numThreads, NUM_RSS_KEYS, EFS) -> (NUM_RSS_KEYS, EFS) (server.cpp:432-441)."""
+    return _assemble("assembleMultipartyDPFQueryThreadResults", server, parts)
+
+
+def calcMultiPartyOptDPFKeyLength(p, log_domain_size, t):
+    """utils.cpp:105-116."""
+    return _lib.load().calcMultiPartyOptDPFKeyLength(p, log_domain_size, t)
 
 
 def _assemble(fn, server, parts):

@@ -15,6 +15,11 @@
  *                                                                           server.cpp:505-549
  *   pir_engine_eval_all              evalAllOptimizedDPF                    dpf_tree.cpp:473-598
  *   pir_engine_answer_coefs[_dev]    runHollantiQuery / ...Thread           server.cpp:321-371
+ *   pir_engine_answer_mp[_dev]       runOptimizedMultiPartyDPFQuery[Thread] server.cpp:136-176,
+ *                                    (evalAllOptMultiPartyDPF[Thread])      :384-430,
+ *                                                                 multiparty_dpf.cpp:467-615
+ *   pir_engine_mp_key_len            calcMultiPartyOptDPFKeyLength          utils.cpp:105-116
+ *   pir_engine_mp_num_keys           NUM_RSS_KEYS                           params.cpp:618
  *   pir_engine_key_len               calcOptimizedDPFTreeKeyLength          utils.cpp:85-90
  *   pir_comm_* + partitions          (new) split-shard across GPUs, XOR all-reduce over RCCL
  */
@@ -103,6 +108,24 @@ int pir_engine_answer_coefs(pir_engine_t *e, const uint8_t *const *coefs, uint64
 /* device form: round a's coefficient of engine row r at d_coefs[a * coef_pitch + r] */
 int pir_engine_answer_coefs_dev(pir_engine_t *e, const uint8_t *d_coefs, uint64_t coef_pitch,
                                 uint64_t row0, uint64_t nrows, uint8_t *d_result, void *stream);
+/* Multiparty sqrt(N) DPF answer of party index 1..p with threshold t (the engine must have
+ * num_rounds == pir_engine_mp_num_keys(p, t), one output share per round):
+ *   result[a] = XOR_{r in rows} share[a][r] * shard row r,   a < NUM_RSS_KEYS,
+ *   share[a][i*mu + x] = XOR_{j: toggle[a][i][j] != 0} G(seed[i][j], mu)[x] ^ cw[j][x]
+ * over the key layout of multiparty_dpf.cpp:133-273 / :467-539 (seeds, toggle bytes, correction
+ * words; mu = 2^ceil(log2(ceil(2^(n/2) * 2^((p-1)/2)))) records per row, nu = 2^n / mu rows).
+ * rows: the thread slice [thread_num*S*mu, (thread_num+1)*S*mu), S = nu / num_threads, of
+ * runOptimizedMultiPartyDPFQueryThread (num_threads = 1: the whole domain), within this engine's
+ * partition.  key_bytes >= pir_engine_mp_eval_bytes(p, n, t) (the bytes the evaluation reads;
+ * calcMultiPartyOptDPFKeyLength sizes the buffer the Go client sends).  Always the honest
+ * answer (the Byzantine branch of server.cpp:157-160 is the caller's). */
+int pir_engine_answer_mp(pir_engine_t *e, const uint8_t *key, uint64_t key_bytes, int p, int t,
+                         int thread_num, int num_threads, uint8_t *result);
+int pir_engine_answer_mp_dev(pir_engine_t *e, const uint8_t *d_key, int p, int t, int thread_num,
+                             int num_threads, uint8_t *d_result, void *stream);
+int pir_engine_mp_num_keys(int p, int t);
+int pir_engine_mp_key_len(int p, int n, int t);
+long long pir_engine_mp_eval_bytes(int p, int n, int t); /* -1: no layout for (p, n, t) */
 /* DPF shares of this engine's rows: out[a*R + i] (dataShare[a][i]) */
 int pir_engine_eval_all(pir_engine_t *e, const uint8_t *key, uint8_t *out);
 

@@ -11,8 +11,11 @@
  *                                      partial answer over rows [t*N/T,(t+1)*N/T); the reference
  *                                      body is defective)
  *   assemblDPFTreeQueryThreadResults   server.h:53,     server.cpp:553-562
- *   setSystemParams / freeParams       params.h:63-64,  params.cpp:467-642 (tree and Hollanti
- *                                      modes; the others abort)
+ *   setSystemParams / freeParams       params.h:63-64,  params.cpp:467-642 (tree, multiparty and
+ *                                      Hollanti modes; the others abort)
+ *   runOptimizedMultiPartyDPFQuery[Thread], assembleMultipartyDPFQueryThreadResults
+ *                                      server.h:37,46,52, server.cpp:136-176, :384-441
+ *   calcMultiPartyOptDPFKeyLength      utils.h,         utils.cpp:105-116
  *   runHollantiQuery[Thread], assemble*QueryThreadResults, the other modes' entry points (abort)
  *                                      server.h:39-53,  server.cpp:304-665
  *   encode_within_files_server         client.h:29,     client.cpp:93-110
@@ -76,7 +79,8 @@ extern int D;
 extern int MAC_SIZE_BYTES;
 extern int CHECK_MAC;
 /* globals of the other PIR modes (params.h:39-54), read by the Go mode handlers
- * (src/server_util/{multiparty,cd732,woodruff}.go); those modes are not served (see below) */
+ * (src/server_util/{multiparty,cd732,woodruff}.go); NUM_RSS_KEYS = the multiparty answer's
+ * share count (params.cpp:603-619), the others' modes are not served (see below) */
 extern int NUM_RSS_KEYS;
 extern int NUM_CD_KEYS;
 extern int WOODRUFF_M;
@@ -104,21 +108,31 @@ void runHollantiQueryThread(server *s, uint8_t **keys, int threadNum, int startI
                             uint8_t **result);
 void assembleHollantiQueryThreadResults(server *s, uint8_t ***in, int numThreads, uint8_t **out);
 
-/* ---- the other PIR modes' server entry points, bound by src/server_util/*.go
- *      (shamir.go:52, multiparty.go:64, cd732.go:64, woodruff.go:69).  Their modes are outside
- *      this engine's scope: setSystemParams refuses modes 1, 2, 4, 5, 6, and these abort with a
- *      message if reached anyway.  The assemble functions are the reference's XOR folds
- *      (server.cpp:304-319, 432-441, 494-503, 647-665). ---- */
-void runOptShamirDPFQueryThread(server *s, uint8_t **keys, int threadNum, int startIndex,
-                                int endIndex, uint8_t **result);
+/* ---- multiparty sqrt(N) DPF PIR (mode 1): evalAllOptMultiPartyDPF[Thread]
+ *      (multiparty_dpf.cpp:467-615) + the GF(2^8) scan, on the engine (pir_engine_answer_mp).
+ *      key = calcMultiPartyOptDPFKeyLength(NUM_PARTIES, LOG_NUM_ENCODED_FILES, T) bytes (the
+ *      evaluation reads the layout of multiparty_dpf.cpp:133-273, which fits inside it);
+ *      result[a], a < NUM_RSS_KEYS, = ENCODED_FILE_SIZE_BYTES.  The Thread form answers rows
+ *      [threadNum*S*mu, (threadNum+1)*S*mu), S = nu / numThreads (server.cpp:401-423); its
+ *      Byzantine branch is the honest answer in the reference too. ---- */
+int calcMultiPartyOptDPFKeyLength(int p, int log_domainSize, int t);
+void runOptimizedMultiPartyDPFQuery(server *s, uint8_t *key, uint8_t **result);
 void runOptimizedMultiPartyDPFQueryThread(server *s, uint8_t *key, int threadNum, int numThreads,
                                           uint8_t **result);
+void assembleMultipartyDPFQueryThreadResults(server *s, uint8_t ***in, int numThreads,
+                                             uint8_t **out);
+
+/* ---- the other PIR modes' server entry points, bound by src/server_util/ (shamir.go:52,
+ *      cd732.go:64, woodruff.go:69).  Their modes are outside this engine's scope:
+ *      setSystemParams refuses modes 2, 4, 5, 6, and these abort with a message if reached
+ *      anyway.  The assemble functions are the reference's XOR folds (server.cpp:304-319,
+ *      494-503, 647-665). ---- */
+void runOptShamirDPFQueryThread(server *s, uint8_t **keys, int threadNum, int startIndex,
+                                int endIndex, uint8_t **result);
 void runCDQueryThread(server *s, uint8_t *key, int threadNum, int numThreads, uint8_t **result);
 void runWoodruffQueryThread(server *s, uint8_t *key, int threadNum, int startIndex, int endIndex,
                             uint8_t **result);
 void assembleShamirQueryThreadResults(server *s, uint8_t ***in, int numThreads, uint8_t **out);
-void assembleMultipartyDPFQueryThreadResults(server *s, uint8_t ***in, int numThreads,
-                                             uint8_t **out);
 void assembleCDQueryThreadResults(server *s, uint8_t ***in, int numThreads, uint8_t **out);
 void assembleWoodruffQueryThreadResults(server *s, uint8_t ***in, int numThreads, uint8_t **out);
 /* utils.h:29-30 */

@@ -6,6 +6,7 @@
  */
 #include "pir_oracle.h"
 
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -111,6 +112,8 @@ void orc_G(const uint8_t seed[16], uint32_t plen, uint8_t *out) {
         memset(ctr, 0, 16);
         ctr[15] = (uint8_t)j;
         ctr[14] = (uint8_t)(j >> 8);
+        ctr[13] = (uint8_t)(j >> 16);
+        ctr[12] = (uint8_t)(j >> 24);
         aes_encrypt_rk(rk, ctr, blk);
         uint32_t m = plen - off < 16 ? plen - off : 16;
         memcpy(out + off, blk, m);
@@ -412,4 +415,53 @@ void orc_decode(int p, int k, int r, int rho, int nq, int efs, const uint8_t *er
     }
     memcpy(out, acc, efs); /* FILE_SIZE_BYTES (no MAC) == efs in tree mode */
     free(acc); free(pts); free(sh); free(tmp);
+}
+
+/* ---- multiparty sqrt(N) DPF ---------------------------------------------------------------- */
+int orc_choose(int n, int k) { return k == 0 ? 1 : (n * orc_choose(n - 1, k - 1)) / k; } /* utils.cpp:168 */
+
+void orc_mp_sizes(int p, int n, int t, uint64_t *o) {
+    int q = orc_choose(p, t);
+    uint64_t nrk = (uint64_t)(q * (p - t) / p), p2 = 1ull << (q - 1);        /* params.cpp:618 */
+    int mu_pow = (int)ceil(log2(ceil(pow(2, n / 2.0) * pow(2, (p - 1) / 2.0)))); /* :473 */
+    uint64_t mu = 1ull << mu_pow, nu = mu_pow > n ? 0 : 1ull << (n - mu_pow);
+    o[0] = nrk; o[1] = p2; o[2] = mu; o[3] = nu;
+    o[4] = 16 * p2 * nu + nrk * nu * p2 + p2 * mu;       /* seeds | toggle bytes | cw (:485-511) */
+    uint64_t kmu = 1ull << (n / 2), knu = 1ull << (n - n / 2);               /* utils.cpp:111-113 */
+    o[5] = (uint64_t)(int)(16 * p2 * knu + nrk * knu * p2 + p2 * kmu);
+}
+
+void orc_mp_eval(int p, int n, int t, const uint8_t *key, int thread_num, int num_threads,
+                 uint8_t *out) {
+    uint64_t z[6];
+    orc_mp_sizes(p, n, t, z);
+    const uint64_t nrk = z[0], p2 = z[1], mu = z[2], nu = z[3], N = 1ull << n;
+    const uint64_t tog = nu * 16 * p2, cw = tog + nrk * nu * p2, slice = nu / num_threads;
+    uint8_t *g = malloc(mu);
+    memset(out, 0, nrk * N);
+    for (uint64_t i = thread_num * slice; i < (thread_num + 1) * slice; i++)   /* :590-601 */
+        for (uint64_t j = 0; j < p2; j++) {
+            orc_G(key + i * 16 * p2 + 16 * j, (uint32_t)mu, g);
+            for (uint64_t a = 0; a < nrk; a++) {
+                if (!key[tog + a * nu * p2 + i * p2 + j]) continue;
+                uint8_t *o = out + a * N + i * mu;
+                for (uint64_t x = 0; x < mu; x++) o[x] ^= g[x] ^ key[cw + j * mu + x];
+            }
+        }
+    free(g);
+}
+
+void orc_mp_answer(int p, int t, int n, int efs, const uint8_t *key, const uint8_t *shard,
+                   int thread_num, int num_threads, uint8_t *result) {
+    uint64_t z[6];
+    orc_mp_sizes(p, n, t, z);
+    const uint64_t nrk = z[0], mu = z[2], nu = z[3], N = 1ull << n, slice = nu / num_threads;
+    uint8_t *c = malloc(nrk * N);
+    orc_mp_eval(p, n, t, key, thread_num, num_threads, c);
+    memset(result, 0, nrk * efs);
+    for (uint64_t i = thread_num * slice * mu; i < (thread_num + 1) * slice * mu; i++) /* :416-422 */
+        for (int b = 0; b < efs; b++)
+            for (uint64_t a = 0; a < nrk; a++)
+                result[a * efs + b] ^= orc_gf_mul(c[a * N + i], shard[i * (uint64_t)efs + b]);
+    free(c);
 }

@@ -11,6 +11,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stdio.h>
 #include <time.h>
 #include <thread>
 #include <vector>
@@ -19,6 +20,7 @@
 #include "coding.h"
 #include "params.h"
 #include "dpf_tree.h"
+#include "multiparty_dpf.h"
 #include "server.h"
 #include "client.h"
 
@@ -356,5 +358,68 @@ void ref_hollanti_sizes(int L, int f, int t, int k, int r, int rho, int* out3) {
 }
 
 int ref_shamir_key_len(int n) { return calcShamirDPFKeyLength(n); }
+
+// ---- multiparty sqrt(N) DPF (mode 1) --------------------------------------------------------
+// utils.cpp:105-116
+int ref_mp_key_len(int p, int n, int t) { return calcMultiPartyOptDPFKeyLength(p, n, t); }
+
+// setSystemParams(L,f,t,k,r,b,rho,0,mode=1) sizing: p, n, efs, NUM_RSS_KEYS, key length
+void ref_mp_sizes(int L, int f, int t, int k, int r, int b, int rho, int* out5) {
+    setSystemParams(L, f, t, k, r, b, rho, 0, 1);
+    out5[0] = NUM_PARTIES;
+    out5[1] = LOG_NUM_ENCODED_FILES;
+    out5[2] = ENCODED_FILE_SIZE_BYTES;
+    out5[3] = NUM_RSS_KEYS;
+    out5[4] = calcMultiPartyOptDPFKeyLength(NUM_PARTIES, LOG_NUM_ENCODED_FILES, T);
+}
+
+// multiparty_dpf.cpp:467-539 (num_threads == 0) or the Thread form :541-615 for one thread;
+// out is nrk x 2^n (dataShare[a][r])
+void ref_mp_eval(int p, int n, int t, int nrk, const uint8_t* key, int thread_num,
+                 int num_threads, uint8_t* out) {
+    NUM_RSS_KEYS = nrk;
+    EVP_CIPHER_CTX* ctx = EVP_CIPHER_CTX_new();
+    size_t N = (size_t)1 << n;
+    std::vector<uint8_t*> ds(nrk);
+    for (int a = 0; a < nrk; a++) ds[a] = out + a * N;
+    if (num_threads == 0)
+        evalAllOptMultiPartyDPF(ctx, p, n, (uint8_t*)key, t, ds.data());
+    else
+        evalAllOptMultiPartyDPFThread(ctx, p, n, (uint8_t*)key, t, ds.data(), thread_num,
+                                      num_threads);
+    EVP_CIPHER_CTX_free(ctx);
+}
+
+// server.cpp:136-176 (num_threads == 0) or num_threads runOptimizedMultiPartyDPFQueryThread
+// calls + assembleMultipartyDPFQueryThreadResults (server.cpp:384-441) on a resident server
+// (ref_server_new with nq = nrk); result is nrk x efs
+void ref_mp_server_answer(void* hv, int p, int t, int nrk, const uint8_t* key, int num_threads,
+                          uint8_t* result) {
+    ref_srv* h = (ref_srv*)hv;
+    set_tree_globals(h->p, h->n, h->efs, h->nq);
+    NUM_PARTIES = p;
+    T = t;
+    NUM_RSS_KEYS = nrk;
+    std::vector<uint8_t*> res(nrk);
+    for (int a = 0; a < nrk; a++) res[a] = result + (size_t)a * h->efs;
+    if (num_threads == 0) {
+        runOptimizedMultiPartyDPFQuery(&h->s, (uint8_t*)key, res.data());
+        return;
+    }
+    if (num_threads > h->s.numThreads) {  // one EVP context per thread (server.cpp:393)
+        fprintf(stderr, "ref_mp_server_answer: server built with %d threads\n", h->s.numThreads);
+        abort();
+    }
+    std::vector<std::vector<std::vector<uint8_t>>> buf(
+        num_threads, std::vector<std::vector<uint8_t>>(nrk, std::vector<uint8_t>(h->efs)));
+    std::vector<std::vector<uint8_t*>> rows(num_threads, std::vector<uint8_t*>(nrk));
+    std::vector<uint8_t**> in(num_threads);
+    for (int th = 0; th < num_threads; th++) {
+        for (int a = 0; a < nrk; a++) rows[th][a] = buf[th][a].data();
+        in[th] = rows[th].data();
+        runOptimizedMultiPartyDPFQueryThread(&h->s, (uint8_t*)key, th, num_threads, in[th]);
+    }
+    assembleMultipartyDPFQueryThreadResults(&h->s, in.data(), num_threads, res.data());
+}
 
 }  // extern "C"

@@ -142,3 +142,41 @@ def gf_mul(a, b):
 
 def gf_pow(a, e):
     return lib().orc_gf_pow(a, e)
+
+
+# ---- multiparty sqrt(N) DPF (mode 1) ---------------------------------------------------------
+def mp_sizes(p, n, t):
+    """{nrk, p2, mu, nu, eval_bytes, key_len} (multiparty_dpf.cpp:470-478, utils.cpp:105-116)."""
+    o = (ctypes.c_uint64 * 6)()
+    lib().orc_mp_sizes(p, n, t, o)
+    return dict(zip(("nrk", "p2", "mu", "nu", "eval_bytes", "key_len"), [int(v) for v in o]))
+
+
+def mp_key(p, n, t, seed):
+    """A synthetic multiparty key: xorshift bytes over max(eval_bytes, key_len), with the toggle
+    bytes mapped to {0, 1, the raw byte} (raw % 3), so toggles are both set and clear.  The
+    evaluation is a function of the key bytes: the reference's own key generation cannot make
+    a usable key (RSS_SUBSETS is never filled, params.cpp:613-617)."""
+    z = mp_sizes(p, n, t)
+    key = xorshift(seed, max(z["eval_bytes"], z["key_len"], 16))
+    lo = z["nu"] * 16 * z["p2"]
+    hi = lo + z["nrk"] * z["nu"] * z["p2"]
+    tb = key[lo:hi]
+    key[lo:hi] = np.where(tb % 3 == 0, 0, np.where(tb % 3 == 1, 1, tb))
+    return key
+
+
+def mp_eval(p, n, t, key, thread_num=0, num_threads=1):
+    z = mp_sizes(p, n, t)
+    out = np.zeros(z["nrk"] << n, np.uint8)
+    lib().orc_mp_eval(p, n, t, P(np.ascontiguousarray(key, np.uint8)), thread_num, num_threads,
+                      P(out))
+    return out.reshape(z["nrk"], 1 << n)
+
+
+def mp_answer(p, t, n, efs, key, shard, thread_num=0, num_threads=1):
+    z = mp_sizes(p, n, t)
+    out = np.zeros(z["nrk"] * efs, np.uint8)
+    lib().orc_mp_answer(p, t, n, efs, P(np.ascontiguousarray(key, np.uint8)),
+                        P(np.ascontiguousarray(shard, np.uint8)), thread_num, num_threads, P(out))
+    return out.reshape(z["nrk"], efs)

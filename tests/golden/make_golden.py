@@ -244,12 +244,61 @@ def hollanti():
                             "shamir_key_len": {str(n): REF.ref_shamir_key_len(n) for n in (1, 2, 7, 10, 20, 25)}})
 
 
+MP_CASES = [  # (p, t, n, efs, threads): shares per record 2/3/4/5/9, short rows, mu_pow > n
+    (3, 1, 10, 64, 4), (3, 1, 11, 37, 2), (4, 1, 12, 48, 8), (4, 2, 9, 20, 1), (3, 1, 4, 16, 1),
+    (3, 1, 3, 8, 1), (5, 1, 10, 32, 2), (3, 2, 10, 64, 1), (6, 1, 8, 16, 2), (7, 1, 4, 8, 1),
+    (10, 1, 10, 16, 1)]
+
+
+def mp():
+    """Multiparty sqrt(N) DPF server path (mode 1) on synthetic keys (tests/_oracle.mp_key: the
+    reference's own keygen leaves the toggle bytes unset): the shares of evalAllOptMultiPartyDPF
+    and of its Thread form, runOptimizedMultiPartyDPFQuery, and the thread-assembled answer."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    REF.ref_mp_key_len.restype = ctypes.c_int
+    cases = []
+    for (p, t, n, efs, T) in MP_CASES:
+        z = O.mp_sizes(p, n, t)
+        nrk, N = z["nrk"], 1 << n
+        assert REF.ref_mp_key_len(p, n, t) == z["key_len"]
+        kseed, sseed = 0x5EED0000 + 97 * n + p, 0xD00D0000 + 13 * n + t
+        key = O.mp_key(p, n, t, kseed)
+        shard = O.xorshift(sseed, N * efs)
+        shares = np.zeros(nrk * N, np.uint8)
+        REF.ref_mp_eval(p, n, t, nrk, ptr(key), 0, 0, ptr(shares))
+        thr_shares = []
+        for th in range(T):
+            o = np.zeros(nrk * N, np.uint8)
+            REF.ref_mp_eval(p, n, t, nrk, ptr(key), th, T, ptr(o))
+            thr_shares.append(sha(o))
+        h = REF.ref_server_new(p, 1, n, efs, nrk, ptr(shard), 0, T)
+        ans = np.zeros(nrk * efs, np.uint8)
+        REF.ref_mp_server_answer(ctypes.c_void_p(h), p, t, nrk, ptr(key), 0, ptr(ans))
+        tans = np.zeros(nrk * efs, np.uint8)
+        REF.ref_mp_server_answer(ctypes.c_void_p(h), p, t, nrk, ptr(key), T, ptr(tans))
+        REF.ref_server_free(ctypes.c_void_p(h))
+        cases.append({"p": p, "t": t, "n": n, "efs": efs, "threads": T, "key_seed": kseed,
+                      "shard_seed": sseed, "sizes": z, "key_sha256": sha(key),
+                      "shares_sha256": sha(shares), "thread_shares_sha256": thr_shares,
+                      "answer": ans.tobytes().hex(), "thread_answer": tans.tobytes().hex()})
+        print("mp case", p, t, n, efs, T, z)
+    sizes = []
+    for (L, f, t, k, r, b, rho) in [(10, 64, 1, 1, 1, 0, 1), (12, 100, 1, 2, 1, 0, 1),
+                                    (11, 48, 2, 1, 1, 0, 1), (10, 32, 1, 1, 0, 1, 1)]:
+        s = (ctypes.c_int * 5)()
+        REF.ref_mp_sizes(L, f, t, k, r, b, rho, s)
+        sizes.append({"L": L, "f": f, "t": t, "k": k, "r": r, "b": b, "rho": rho,
+                      "p": s[0], "n": s[1], "efs": s[2], "nrk": s[3], "key_len": s[4]})
+    write("multiparty.json", {"cases": cases, "setup_sizes": sizes})
+
+
 if __name__ == "__main__":
     REF.ref_server_new.restype = ctypes.c_void_p
     REF.ref_blen.restype = ctypes.c_uint32
     for fn in (REF.ref_gf_mul, REF.ref_gf_pow, REF.ref_gf_inv):
         fn.restype = ctypes.c_uint8
-    what = sys.argv[1:] or ["prg", "gf", "dpf", "e2e", "thread", "fullsize", "hollanti"]
+    what = sys.argv[1:] or ["prg", "gf", "dpf", "e2e", "thread", "fullsize", "hollanti", "mp"]
     if "prg" in what: prg_kats()
     if "gf" in what: gf_kats()
     if "dpf" in what: dpf_and_answers()
@@ -257,3 +306,4 @@ if __name__ == "__main__":
     if "thread" in what: thread_defect()
     if "fullsize" in what: fullsize()
     if "hollanti" in what: hollanti()
+    if "mp" in what: mp()
