@@ -36,6 +36,7 @@ core over one shared copy of the shard).
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 import tempfile
@@ -65,6 +66,12 @@ CONFIGS = {
 COEF_CONFIGS = {
     "ch": (24, 1024, 1, "polynomial (Hollanti) PIR: 2^24 x 1 KiB shard, 1 round, explicit coefficient vector"),
     "ch3": (24, 1024, 3, "polynomial (Hollanti) PIR: 2^24 x 1 KiB shard, 3 rounds (k=3), explicit coefficient vectors"),
+}
+# multiparty sqrt(N) DPF answers: a step = one query's key (device-resident) evaluated into
+# NUM_RSS_KEYS shares and scanned against the shard (server.cpp:136-176)
+MP_CONFIGS = {
+    "cm": (24, 1024, 3, 1, "multiparty sqrt(N) DPF PIR (mode 1): 2^24 x 1 KiB shard, p=3, t=1 (2 shares, 4 seeds per row of 8192 records)"),
+    "cm4": (24, 1024, 4, 1, "multiparty sqrt(N) DPF PIR (mode 1): 2^24 x 1 KiB shard, p=4, t=1 (3 shares, 8 seeds per row of 8192 records)"),
 }
 # batched configs: a step answers `batch` keys (distinct indices) against the shard
 BATCH_CONFIGS = {
@@ -435,7 +442,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default=None,
-                    choices=sorted(CONFIGS) + sorted(BATCH_CONFIGS) + sorted(COEF_CONFIGS),
+                    choices=sorted(CONFIGS) + sorted(BATCH_CONFIGS) + sorted(COEF_CONFIGS) + sorted(MP_CONFIGS),
                     help="default: c24 on one GPU, c4 (split shard) on several")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=20.0,
@@ -478,6 +485,8 @@ def main():
         return run_batch(args, ctx, config)
     if config in COEF_CONFIGS:
         return run_coefs(args, ctx, config)
+    if config in MP_CONFIGS:
+        return run_mp(args, ctx, config)
     n_cfg, efs, p, nq, strong, workload = CONFIGS[config]
     g = log2_exact(world)
     n = n_cfg if strong else n_cfg + g  # logical tree depth
@@ -689,6 +698,73 @@ def run_coefs(args, ctx, config):
                         "traffic": None, "algorithmic_bytes_per_query": int(algo),
                         "note": "wall time per query over the device work of all three launches"},
            "parity": {"coefficient_linearity": ok}}
+    if ctx.rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def run_mp(args, ctx, config):
+    """Multiparty sqrt(N) DPF answers (answer_mp_dev): each step evaluates one query's key into
+    its NUM_RSS_KEYS shares (k_mp_shares) and scans them against the shard.  Keys are random
+    bytes in the evaluation's layout (toggle bytes 0/1): the reference's own key generation
+    leaves them unset (params.cpp:613-617).  N = 1 only (replicas on more GPUs)."""
+    import erasurecodedpir_amd as pir
+    n, efs, p, t, workload = MP_CONFIGS[config]
+    N = 1 << n
+    nrk = pir.mp_num_keys(p, t)
+    eb = pir.mp_eval_bytes(p, n, t)
+    rng = np.random.default_rng(11)
+    K, W = args.steps, args.warmup
+    nkeys = max(2, min(K, 4))
+    mu = 1 << int(np.ceil(np.log2(np.ceil(2 ** (n / 2) * 2 ** ((p - 1) / 2)))))
+    nu, p2 = N // mu, 1 << (math.comb(p, t) - 1)
+    tog = nu * 16 * p2
+    keys = rng.integers(0, 256, (nkeys, eb), dtype=np.uint8)
+    keys[:, tog:tog + nrk * nu * p2] = rng.integers(0, 2, (nkeys, nrk * nu * p2), dtype=np.uint8)
+    eng = pir.Engine(2, 1, n, efs, nrk, device=ctx.local)
+    eng.fill_shard_random(SHARD_SEED)
+    d_k = eng.alloc_dev(nkeys * eb)
+    d_r = eng.alloc_dev(K * nrk * efs)
+    eng.h2d(d_k, keys.reshape(-1))
+    for i in range(W):
+        eng.answer_mp_dev(d_k + (i % nkeys) * eb, p, t, d_r)
+    dt = ctx.timed(eng, lambda: [eng.answer_mp_dev(d_k + (i % nkeys) * eb, p, t,
+                                                   d_r + i * nrk * efs) for i in range(K)])
+    ms = dt / K * 1e3
+    # correctness at full size: flipping cw[j][x] by d moves share a's answer by
+    # d * XOR of the records i*mu + x of the rows whose toggle (a, i, j) is set
+    j, x, d = 1, 777, 0x5A
+    cwo = tog + nrk * nu * p2
+    k0 = keys[0].copy()
+    base = eng.answer_mp(k0, p, t)
+    k0[cwo + j * mu + x] ^= d
+    moved = eng.answer_mp(k0, p, t)
+    tab = _gf_table(d)
+    ok = True
+    for a in range(nrk):
+        acc = np.zeros(efs, np.uint8)
+        for i in range(nu):
+            if keys[0][tog + a * nu * p2 + i * p2 + j]:
+                acc ^= eng.shard_row(i * mu + x)
+        ok &= bool(np.array_equal((base ^ moved)[a], tab[acc]))
+    dev0 = eng.d2h(d_r, nrk * efs).reshape(nrk, efs)
+    ok_dev = bool(np.array_equal(dev0, eng.answer_mp(keys[0], p, t)))
+    eng.close()
+    gib = float(N) * efs / GIB
+    algo = float(N) * efs + eb  # shard + the key
+    out = {"metric": METRIC, "value": round(gib / (ms / 1e3), 3), "unit": "GiB/s", "n_gpus": 1,
+           "steps": K, "warmup": W, "ms_per_step": r5(ms), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+           "config": {"workload": workload, "records": N, "record_bytes": efs, "parties": p,
+                      "threshold": t, "shares": nrk, "seeds_per_row": p2, "row_records": mu,
+                      "rows": nu, "key_bytes_read": eb,
+                      "step": "one query: k_mp_shares (AES-CTR per seed, toggled into the shares) "
+                              "+ k_scan + k_reduce"},
+           "roofline": {"bound": "hbm", "kernel": "k_mp_shares + k_scan + k_reduce",
+                        "achieved": round(algo / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": None, "algorithmic_bytes_per_query": int(algo),
+                        "note": "wall time per query over the device work of all three launches"},
+           "parity": {"correction_word_linearity": ok, "device_equals_host_api": ok_dev}}
     if ctx.rank == 0:
         print(json.dumps(out), flush=True)
 

@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpir_engine.so")
+# $PIR_ENGINE_LIB: another build of the same library (A/B diagnostics only)
+LIB_PATH = os.environ.get("PIR_ENGINE_LIB") or os.path.join(_HERE, "libpir_engine.so")
 
 c_u8_p = ctypes.POINTER(ctypes.c_uint8)
 

@@ -468,6 +468,12 @@ typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 #ifndef PIR_PLANE_U
 #define PIR_PLANE_U 8
 #endif
+// k_query: rounds up to which the scan waves fold with scalar branches instead of plane-table
+// masks.  Branches measured slower at 5 rounds (c5: 8.36 vs 6.34 ms per query; the k_query scan
+// waves are too few per SIMD to hide the scalar issue), so only 1-2 rounds take them.
+#ifndef PIR_QUERY_BRANCH_MAXNQ
+#define PIR_QUERY_BRANCH_MAXNQ 2
+#endif
 
 // Many-round scan with wave-uniform coefficients: the 8 masks of coefficient byte c come from
 // the table with one s_load_dwordx8, and one asm statement per round folds a row's 2 dwords
@@ -629,6 +635,133 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
   __syncthreads();  // red[] zeroed
   if (active) {
     const uint32_t wbase = (UNI ? (uint32_t)lane : chunk) * VEC;
+#pragma unroll
+    for (int a = 0; a < NQ; ++a)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        uint32_t acc = Z[a][7][v];
+#pragma unroll
+        for (int k = 6; k >= 0; --k) acc = gf_xtime4(acc) ^ Z[a][k][v];
+        if (acc) atomicXor(&red[a * GW + wbase + v], acc);
+      }
+  }
+  __syncthreads();
+  uint32_t* slab = reinterpret_cast<uint32_t*>(slabs) +
+                   ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * (NQ * GW);
+  if (accumulate)
+    for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) slab[i] ^= red[i];
+  else
+    for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) slab[i] = red[i];
+}
+
+// k_scan_uni: the scan for records of at least one wave row (one record per wave row,
+// wave-uniform coefficients), with the scan-wave inner loop of k_query: a rolling pipeline of U
+// rows per lane (row j + U is loaded into x[u] as soon as row j is folded, so U rows stay in
+// flight), coefficients read 64 rows ahead (lane l loads row r0 + 64 + l's bytes, broadcast by
+// v_readlane), and per round
+//   VEC = 4 (NQ <= 3) or NQ <= 2 : scalar branches on the coefficient bits (~4 v_xor of two
+//             VGPRs per dword instead of 8 v_bitop3 with an SGPR mask, which issue at 2/3 the
+//             rate: profiles/r02_micro/valu_rate.log),
+//   VEC = 2, NQ >= 3 : the 8 plane masks from the table (s_load_dwordx8, one round ahead),
+//   else    : SGPR masks (v_bitop3).
+// Wave w folds rows [w * nrec / nwaves, (w + 1) * nrec / nwaves) of its column group.
+template <int NQ, int NRP, int VEC>
+__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(kScanThreads / 64 * kScanBlocksPerCU / 4)))
+void k_scan_uni(const uint8_t* __restrict__ shard,
+                                                           uint64_t nrec, uint32_t pitch,
+                                                           uint32_t cpr, const uint8_t* __restrict__ c,
+                                                           uint8_t* __restrict__ slabs, int accumulate) {
+  constexpr int CH = VEC * 4;
+  constexpr int GW = kColGroupLanes * VEC;
+  constexpr int U = NQ <= 2 ? 8 : 4;  // divides 64 (the coefficient block)
+  constexpr bool kBranch = VEC == 4 || NQ <= 2;
+  constexpr bool kAsm = !kBranch && VEC == 2 && NQ >= 3;
+  __shared__ uint32_t red[NQ * GW];
+  for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) red[i] = 0;
+
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t waves_per_block = blockDim.x >> 6;
+  const uint64_t wave = (uint64_t)blockIdx.x * waves_per_block + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * waves_per_block;
+  const uint32_t chunk = blockIdx.y * kColGroupLanes + lane;
+  const bool active = chunk < cpr;
+  const uint64_t r0 = wave * nrec / nwaves, r1 = (wave + 1) * nrec / nwaves;
+
+  uint32_t Z[NQ][8][VEC];
+#pragma unroll
+  for (int a = 0; a < NQ; ++a)
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) Z[a][k][v] = 0;
+
+  if (r1 > r0) {
+    // inactive lanes read the row's first chunk (their planes are never written out); slots past
+    // the wave's last row re-read its first row (never folded)
+    const uint8_t* base = shard + (uint64_t)(active ? chunk : 0u) * CH;
+    auto load_row = [&](uint64_t r, Chunk<VEC>& dst) __attribute__((always_inline)) {
+      dst = load_chunk<VEC>(base + (r < r1 ? r : r0) * pitch);
+    };
+    auto coefs64 = [&](uint64_t rb) __attribute__((always_inline)) {
+      const uint64_t r = rb + lane;
+      return r < r1 ? load_coef<NRP>(c, r) : make_uint4(0, 0, 0, 0);
+    };
+    Chunk<VEC> x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load_row(r0 + u, x[u]);
+    uint4 c4 = coefs64(r0);
+    for (uint64_t rb = r0; rb < r1; rb += 64) {
+      const uint4 c4n = coefs64(rb + 64);  // the next 64 rows' coefficients, in flight
+      const uint32_t nb = (uint32_t)(r1 - rb < 64 ? r1 - rb : 64);
+      for (uint32_t j0 = 0; j0 < nb; j0 += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t j = j0 + u;
+          if (j < nb) {  // wave-uniform
+            const uint4 cf = make_uint4(__builtin_amdgcn_readlane(c4.x, j),
+                                        NRP > 4 ? __builtin_amdgcn_readlane(c4.y, j) : 0u,
+                                        NRP > 8 ? __builtin_amdgcn_readlane(c4.z, j) : 0u,
+                                        NRP > 8 ? __builtin_amdgcn_readlane(c4.w, j) : 0u);
+            if constexpr (kAsm) {
+              u32x8 m = plane_masks_issue(coef_byte(cf, 0));
+#pragma unroll
+              for (int a = 0; a < NQ; ++a) {
+                auto& Za = reinterpret_cast<uint32_t(&)[8][2]>(Z[a]);
+                if (a + 1 < NQ) m = planes_fold2_next(Za, x[u].v[0], x[u].v[1], m, coef_byte(cf, a + 1));
+                else planes_fold2(Za, x[u].v[0], x[u].v[1], m);
+              }
+            } else {
+#pragma unroll
+              for (int a = 0; a < NQ; ++a) {
+                const uint32_t ca = coef_byte(cf, a);
+                if constexpr (kBranch) {
+#pragma unroll
+                  for (int kk = 0; kk < 8; ++kk)
+                    if (ca & (1u << kk)) {
+#pragma unroll
+                      for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= x[u].v[v];
+                    }
+                } else {
+#pragma unroll
+                  for (int kk = 0; kk < 8; ++kk) {
+                    const uint32_t m = 0u - ((ca >> kk) & 1u);
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v) Z[a][kk][v] = mxor(Z[a][kk][v], x[u].v[v], m);
+                  }
+                }
+              }
+            }
+          }
+          load_row(rb + j + U, x[u]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      c4 = c4n;
+    }
+  }
+  __syncthreads();  // red[] zeroed
+  if (active) {
+    const uint32_t wbase = lane * VEC;
 #pragma unroll
     for (int a = 0; a < NQ; ++a)
 #pragma unroll
@@ -1318,8 +1451,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
 #pragma unroll
         for (int v = 0; v < VEC; ++v) Z[a][kk][v] = 0;
     const uint32_t ngroups = (TILE + rpw - 1) / rpw;
-    // many rounds, wave-uniform coefficients, 2 dwords per lane: masks from the plane table
-    constexpr bool kPlaneAsm = UNI && VEC == 2 && NQ >= 3;
+    // many rounds, wave-uniform coefficients, 2 dwords per lane: scalar branches on the
+    // coefficient bits (avg 4 two-VGPR v_xor per dword and round) up to PIR_QUERY_BRANCH_MAXNQ
+    // rounds, else masks from the plane table (8 v_bitop3 with an SGPR mask, 2/3 the issue rate)
+    constexpr bool kPlaneAsm = UNI && VEC == 2 && NQ >= 3 && NQ > PIR_QUERY_BRANCH_MAXNQ;
     // rows in flight per lane (one record per wave row: a rolling pipeline whose x[] stays live
     // across tiles; several records per row: U rows loaded, then folded, per batch)
     constexpr int U = kPlaneAsm ? PIR_PLANE_U : (SW >= 8 ? 8 : 16);
@@ -1347,7 +1482,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
 #pragma unroll
       for (int a = 0; a < NQ; ++a) {
         const uint32_t ca = coef_byte(c4, a);
-        if (UNI && NQ <= 2) {  // scalar branches: ~4 XORs per dword instead of 8 masked
+        if (UNI && NQ <= (PIR_QUERY_BRANCH_MAXNQ > 2 ? PIR_QUERY_BRANCH_MAXNQ : 2)) {  // scalar branches: ~4 XORs per dword instead of 8 masked
 #pragma unroll
           for (int kk = 0; kk < 8; ++kk)
             if (ca & (1u << kk)) {
@@ -2019,7 +2154,7 @@ int final_stage_blocks(const TreePlan& pl) {
   return (int)(st.nin / st.tile);
 }
 
-static int vec_for(int nq) { return nq <= 2 ? 4 : (nq <= 8 ? 2 : 1); }
+static int vec_for(int nq) { return nq <= 3 ? 4 : (nq <= 8 ? 2 : 1); }
 
 ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus, int blocks_per_cu) {
   ScanShape sh{};
@@ -2030,6 +2165,9 @@ ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus, in
   // (wave-uniform coefficients, SGPR masks) beats per-lane coefficients for several records
   if (sh.vec == 2 && pitch / 8 < (uint32_t)kColGroupLanes && pitch / 4 >= (uint32_t)kColGroupLanes)
     sh.vec = 1;
+  if (nq == 3 && sh.vec == 4 && pitch / 16 < (uint32_t)kColGroupLanes &&
+      pitch / 8 >= (uint32_t)kColGroupLanes)
+    sh.vec = 2;  // 3 rounds: a record per wave row at VEC = 2 (as before VEC = 4 took them)
   sh.pitch = pitch;
   sh.cpr = pitch / (sh.vec * 4);
   sh.uniform = sh.cpr >= (uint32_t)kColGroupLanes;
@@ -2049,17 +2187,18 @@ template <int NQ>
 static hipError_t scan_nq(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
                           const uint8_t* d_c, uint8_t* d_slabs, int acc, hipStream_t s) {
   constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : (NQ <= 8 ? 8 : 16)));
-  constexpr int VEC = NQ <= 2 ? 4 : (NQ <= 8 ? 2 : 1);
-  if constexpr (VEC == 2) {
-    if (sh.vec == 1) {
+  constexpr int VEC = NQ <= 3 ? 4 : (NQ <= 8 ? 2 : 1);
+  if constexpr (VEC > 1) {
+    if (sh.vec == VEC / 2) {  // narrower records: one per wave row at half the width
       if (!sh.uniform) return hipErrorInvalidValue;
-      hipLaunchKernelGGL((k_scan<NQ, NRP, 1, true>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
+      hipLaunchKernelGGL((k_scan_uni<NQ, NRP, VEC / 2>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
                          nrec, sh.pitch, sh.cpr, d_c, d_slabs, acc);
       return hipGetLastError();
     }
   }
+  if (sh.vec != VEC) return hipErrorInvalidValue;
   if (sh.uniform)
-    hipLaunchKernelGGL((k_scan<NQ, NRP, VEC, true>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
+    hipLaunchKernelGGL((k_scan_uni<NQ, NRP, VEC>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
                        nrec, sh.pitch, sh.cpr, d_c, d_slabs, acc);
   else
     hipLaunchKernelGGL((k_scan<NQ, NRP, VEC, false>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
