@@ -7,6 +7,13 @@
 //                            here computed on the GPU by pir_engine_encode_across_dev)
 //   TREE_SEARCH_REQUEST (1)  TreeSearchRequest{Key} -> TreeSearchResponse{Results, PartyIndex,
 //                            ServerLatency, ReceiveTime, SendTime}   (tree.go:17-101)
+//   MULTIPARTY_SEARCH_REQUEST (3)  MultipartySearchRequest{Key} -> MultipartySearchResponse{
+//                            Results, ServerLatency, ReceiveTime, SendTime}  (multiparty.go:16-103,
+//                            Mode 1: shares of the sqrt(N) DPF key scanned on the GPU)
+//   HOLLANTI_SEARCH_REQUEST (4)    HollantiSearchRequest{Key [][]byte} -> HollantiSearchResponse{
+//                            Results, ServerLatency, ReceiveTime, SendTime}  (hollanti.go:16-112,
+//                            Mode 3: explicit coefficient vectors scanned on the GPU; the shard
+//                            encoded within files, client.cpp:99-103, on the host)
 //   TEST_REQUEST (7)         TestRequest{Msg} -> TestResponse{Msg}
 // Structs travel as msgpack maps keyed by the Go field names (the go-msgpack MsgpackHandle
 // default).  Durations are int64 nanoseconds; times are msgpack timestamp extensions (-1).
@@ -44,7 +51,10 @@
 
 namespace {
 
-enum : uint8_t { SETUP_REQUEST = 0, TREE_SEARCH_REQUEST = 1, TEST_REQUEST = 7 };  // common.go:147-154
+enum : uint8_t {  // common.go:147-154
+  SETUP_REQUEST = 0, TREE_SEARCH_REQUEST = 1, MULTIPARTY_SEARCH_REQUEST = 3,
+  HOLLANTI_SEARCH_REQUEST = 4, TEST_REQUEST = 7
+};
 
 // ---- msgpack (the subset the protocol uses) ----------------------------------------------
 struct MVal {
@@ -236,7 +246,10 @@ struct Server {
   int party = 1, device = 0, byzantine = 0;
   std::mutex mu;
   pir_engine_t* eng = nullptr;
-  int nq = 0, efs = 0, key_len = 0;  // of the current engine (the params globals may move on)
+  // of the current engine (the params globals may move on): mode, answer rows, record bytes,
+  // tree key length, multiparty (p, t), Hollanti coefficient-vector length
+  int mode = -1, nq = 0, efs = 0, key_len = 0, p = 0, t = 0;
+  uint64_t num_files = 0;
 };
 Server g;
 
@@ -245,10 +258,12 @@ std::string setup(const MVal& req) {  // server.go:295-331
   const int t = (int)req.get_int("T", 1), k = (int)req.get_int("K", 1), r = (int)req.get_int("R");
   const int b = (int)req.get_int("B"), rho = (int)req.get_int("Rho", 1);
   const int mode = (int)req.get_int("Mode"), mac = (int)req.get_int("CheckMAC");
-  if (mode != 0) return "only tree mode (Mode 0) is served by this engine";
+  if (mode != 0 && mode != 1 && mode != 3)
+    return "only the tree (0), multiparty (1) and Hollanti (3) modes are served by this engine";
   if (mac != 0) return "CheckMAC setups are outside this engine's scope";
-  if (t != 1 || b != 0) return "tree mode needs T = 1 and B = 0";
-  if (log_files < 0 || log_files > 40 || fsz < 1 || k < 1 || k > 16 || r < 0 || rho < 1)
+  if (mode == 0 && (t != 1 || b != 0)) return "tree mode needs T = 1 and B = 0";
+  if (mode == 1 && t < 1) return "multiparty mode needs T >= 1";
+  if (log_files < 0 || log_files > 40 || fsz < 1 || k < 1 || k > 16 || r < 0 || rho < 1 || b < 0)
     return "bad setup parameters";
   // the process-global sizing (params.cpp) and the engine change together, under g.mu: a
   // concurrent TREE_SEARCH sees either the old engine and its sizes or the new ones
@@ -256,25 +271,74 @@ std::string setup(const MVal& req) {  // server.go:295-331
   if (g.eng) pir_engine_destroy(g.eng);
   g.eng = nullptr;
   g.key_len = 0;
+  g.mode = -1;
   setSystemParams(log_files, fsz, t, k, r, b, rho, mac, mode);
   if (g.party > NUM_PARTIES) return "this server's party index exceeds NUM_PARTIES";
+  const int rounds = mode == 1 ? NUM_RSS_KEYS : NUM_ROUNDS;
+  if (rounds < 1 || rounds > PIR_MAX_ROUNDS) return "answer rows outside [1,16] (NUM_ROUNDS / NUM_RSS_KEYS)";
   pir_engine_config c{};
   c.device = g.device;
-  c.num_parties = NUM_PARTIES;
-  c.party_index = g.party;
+  // the party count only sizes tree-DPF keys (modes 1 and 3 answer other key forms)
+  c.num_parties = mode == 0 ? NUM_PARTIES : 2;
+  c.party_index = mode == 0 ? g.party : 1;
   c.log_num_records = LOG_NUM_ENCODED_FILES;
   c.record_bytes = (uint32_t)ENCODED_FILE_SIZE_BYTES;
-  c.num_rounds = NUM_ROUNDS;
+  c.num_rounds = rounds;
   c.is_byzantine = g.byzantine || (int)req.get_int("IsByzantine");
   if (pir_engine_create(&c, &g.eng) != PIR_OK) return std::string("engine: ") + pir_engine_last_error();
-  // the synthetic database of client.cpp:16-33, encoded across files on the GPU
-  if (pir_engine_encode_across_dev(g.eng, nullptr, 0, (uint64_t)NUM_FILES, K) != PIR_OK)
-    return std::string("encode: ") + pir_engine_last_error();
-  g.nq = NUM_ROUNDS;
+  if (ENCODE_ACROSS) {
+    // the synthetic database of client.cpp:16-33, encoded across files on the GPU
+    if (pir_engine_encode_across_dev(g.eng, nullptr, 0, (uint64_t)NUM_FILES, K) != PIR_OK)
+      return std::string("encode: ") + pir_engine_last_error();
+  } else {
+    // encoded within files (client.cpp:99-103) on the host by the shim, then uploaded
+    client cl{};
+    server sv{};
+    initialize_client(&cl, (uint8_t)LOG_NUM_FILES, FILE_SIZE_BYTES);
+    initializeServer(&sv, g.party, LOG_NUM_FILES, (uint32_t)ENCODED_FILE_SIZE_BYTES, 0, 1);
+    encode_within_files_server(&cl, &sv);
+    const int rc = pir_engine_set_shard_rows(g.eng, sv.indexList, 0, (uint64_t)NUM_ENCODED_FILES);
+    freeServer(&sv);
+    free_client(&cl);
+    if (rc != PIR_OK) return std::string("upload: ") + pir_engine_last_error();
+  }
+  g.mode = mode;
+  g.nq = rounds;
   g.efs = ENCODED_FILE_SIZE_BYTES;
+  g.p = NUM_PARTIES;
+  g.t = T;
+  g.num_files = (uint64_t)NUM_FILES;
   g.key_len = pir_engine_key_len(c.num_parties, c.log_num_records, c.num_rounds);
   return "";
 }
+
+// msgpack(error) then the search response map: Results [+ PartyIndex], the times
+void write_search(Writer& w, const std::string& err, int nq, int efs, const std::vector<uint8_t>& out,
+                  bool party_index, std::chrono::steady_clock::time_point t0,
+                  std::chrono::system_clock::time_point recv) {
+  err.empty() ? w.nil() : w.str(err);
+  w.map(party_index ? 5 : 4);
+  w.str("Results");
+  if (err.empty()) {
+    w.array((size_t)nq);
+    for (int a = 0; a < nq; ++a) w.bin(out.data() + (size_t)a * efs, (size_t)efs);
+  } else {
+    w.array(0);
+  }
+  if (party_index) {
+    w.str("PartyIndex");
+    w.integer(g.party);
+  }
+  w.str("ServerLatency");
+  w.integer(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                std::chrono::steady_clock::now() - t0).count());
+  w.str("ReceiveTime");
+  w.timestamp(recv);
+  w.str("SendTime");
+  w.timestamp(std::chrono::system_clock::now());
+}
+
+bool is_bytes(const MVal* v) { return v && (v->kind == MVal::BIN || v->kind == MVal::STR); }
 
 void handle(SSL* ssl) {
   Stream in{ssl};
@@ -293,7 +357,8 @@ void handle(SSL* ssl) {
       w.str("ServerLatency");
       w.integer(std::chrono::duration_cast<std::chrono::nanoseconds>(
                     std::chrono::steady_clock::now() - t0).count());
-    } else if (type == TREE_SEARCH_REQUEST) {  // tree.go:17-101
+    } else if (type == TREE_SEARCH_REQUEST || type == MULTIPARTY_SEARCH_REQUEST ||
+               type == HOLLANTI_SEARCH_REQUEST) {  // tree.go:17-101, multiparty.go, hollanti.go
       const MVal* key = req.get("Key");
       std::vector<uint8_t> out;
       int nq = 0, efs = 0;  // this answer's shape, read under the lock with the engine
@@ -301,34 +366,37 @@ void handle(SSL* ssl) {
         std::lock_guard<std::mutex> lk(g.mu);
         nq = g.nq;
         efs = g.efs;
-        if (!g.eng) err = "query before setup";
-        else if (!key || (key->kind != MVal::BIN && key->kind != MVal::STR) ||
-                 (int)key->s.size() != g.key_len)  // the engine's own key length
-          err = "bad key";
-        else {
-          out.resize((size_t)nq * efs);
-          if (pir_engine_answer(g.eng, (const uint8_t*)key->s.data(), out.data()) != PIR_OK)
-            err = std::string("answer: ") + pir_engine_last_error();
+        out.resize((size_t)nq * efs);
+        const int want = type == TREE_SEARCH_REQUEST ? 0 : (type == MULTIPARTY_SEARCH_REQUEST ? 1 : 3);
+        int rc = PIR_OK;
+        if (!g.eng) {
+          err = "query before setup";
+        } else if (g.mode != want) {
+          err = "request does not match the setup's mode";
+        } else if (type == TREE_SEARCH_REQUEST) {
+          if (!is_bytes(key) || (int)key->s.size() != g.key_len)  // the engine's own key length
+            err = "bad key";
+          else
+            rc = pir_engine_answer(g.eng, (const uint8_t*)key->s.data(), out.data());
+        } else if (type == MULTIPARTY_SEARCH_REQUEST) {  // the honest Thread path of multiparty.go:64
+          if (!is_bytes(key))
+            err = "bad key";
+          else
+            rc = pir_engine_answer_mp(g.eng, (const uint8_t*)key->s.data(), key->s.size(), g.p,
+                                      g.t, 0, 1, out.data());
+        } else {  // Key [][]byte: NUM_ROUNDS coefficient vectors of NUM_FILES bytes
+          std::vector<const uint8_t*> ptrs;
+          if (key && key->kind == MVal::ARR && (int)key->a.size() == nq)
+            for (const MVal& v : key->a)
+              if (is_bytes(&v) && v.s.size() == g.num_files) ptrs.push_back((const uint8_t*)v.s.data());
+          if ((int)ptrs.size() != nq)
+            err = "bad key";
+          else
+            rc = pir_engine_answer_coefs(g.eng, ptrs.data(), 0, g.num_files, out.data());
         }
+        if (err.empty() && rc != PIR_OK) err = std::string("answer: ") + pir_engine_last_error();
       }
-      err.empty() ? w.nil() : w.str(err);
-      w.map(5);
-      w.str("Results");
-      if (err.empty()) {
-        w.array((size_t)nq);
-        for (int a = 0; a < nq; ++a) w.bin(out.data() + (size_t)a * efs, (size_t)efs);
-      } else {
-        w.array(0);
-      }
-      w.str("PartyIndex");
-      w.integer(g.party);
-      w.str("ServerLatency");
-      w.integer(std::chrono::duration_cast<std::chrono::nanoseconds>(
-                    std::chrono::steady_clock::now() - t0).count());
-      w.str("ReceiveTime");
-      w.timestamp(recv);
-      w.str("SendTime");
-      w.timestamp(std::chrono::system_clock::now());
+      write_search(w, err, nq, efs, out, type == TREE_SEARCH_REQUEST, t0, recv);
     } else if (type == TEST_REQUEST) {
       const MVal* msg = req.get("Msg");
       w.nil();

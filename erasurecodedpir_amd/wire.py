@@ -14,7 +14,9 @@ import threading
 import msgpack
 import numpy as np
 
-SETUP_REQUEST, TREE_SEARCH_REQUEST, TEST_REQUEST = 0, 1, 7  # common.go:147-154
+# common.go:147-154
+SETUP_REQUEST, TREE_SEARCH_REQUEST, MULTIPARTY_SEARCH_REQUEST, HOLLANTI_SEARCH_REQUEST, TEST_REQUEST = \
+    0, 1, 3, 4, 7
 
 
 class WireError(RuntimeError):
@@ -66,11 +68,13 @@ class Conn:
         self.close()
 
 
-def setup(addr, log_num_files, file_size_bytes, k, r, rho=1, num_threads=1, is_byzantine=0):
-    """SETUP_REQUEST with the fields of common.go:51-65 (tree mode, no MAC)."""
+def setup(addr, log_num_files, file_size_bytes, k, r, rho=1, num_threads=1, is_byzantine=0,
+          mode=0, t=1, b=0):
+    """SETUP_REQUEST with the fields of common.go:51-65 (no MAC): mode 0 tree, 1 multiparty,
+    3 Hollanti."""
     host, port = addr
     req = {"BenchmarkDir": "", "LogNumFiles": log_num_files, "FileSizeBytes": file_size_bytes,
-           "T": 1, "K": k, "R": r, "B": 0, "Rho": rho, "Mode": 0, "IsByzantine": is_byzantine,
+           "T": t, "K": k, "R": r, "B": b, "Rho": rho, "Mode": mode, "IsByzantine": is_byzantine,
            "DelayTime": 0, "NumThreads": num_threads, "CheckMAC": 0}
     with Conn(host, port) as c:
         return c.call(SETUP_REQUEST, req)
@@ -80,6 +84,20 @@ def tree_search(addr, key):
     host, port = addr
     with Conn(host, port) as c:
         return c.call(TREE_SEARCH_REQUEST, {"Key": bytes(key)})
+
+
+def multiparty_search(addr, key):
+    """MULTIPARTY_SEARCH_REQUEST (client/multiparty.go:76-90): Results = NUM_RSS_KEYS answers."""
+    host, port = addr
+    with Conn(host, port) as c:
+        return c.call(MULTIPARTY_SEARCH_REQUEST, {"Key": bytes(key)})
+
+
+def hollanti_search(addr, keys):
+    """HOLLANTI_SEARCH_REQUEST: keys = NUM_ROUNDS coefficient vectors of NUM_FILES bytes."""
+    host, port = addr
+    with Conn(host, port) as c:
+        return c.call(HOLLANTI_SEARCH_REQUEST, {"Key": [bytes(np.asarray(k, np.uint8)) for k in keys]})
 
 
 def tree_query(addrs, index, log_num_files, file_size_bytes, k, r, rho=1, device=0):
