@@ -18,7 +18,13 @@ if [ -z "$SKIP_PROF" ]; then
   rm -rf gpurun_out/prof_default
   step prof_default 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_default -o run --output-format csv -- python bench.py --no-cpu
 fi
-for c in ${EXTRA_CONFIGS:-c5 c3 c3b ch ch3}; do
+for c in ${EXTRA_CONFIGS:-c5 c3 c3b ch ch3 cm cm4}; do
   step bench_$c 300 python bench.py --config $c --steps 10 --warmup 3 --no-cpu --no-extras
 done
+if [ -z "$SKIP_PROF" ]; then  # the coefficient-scan paths: k_mp_shares / k_interleave_coefs + k_scan_uni
+  for c in cm ch3; do
+    rm -rf gpurun_out/prof_$c
+    step prof_$c 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$c -o run --output-format csv -- python bench.py --config $c --steps 10 --warmup 3 --no-cpu --no-extras
+  done
+fi
 exit 0
