@@ -49,6 +49,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "device-resident shard GiB/s per PIR query, 1/2/4/8 MI355X; bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
+# best streaming read of 16 GiB (16-B non-temporal loads, any rows-in-flight / blocks-per-CU
+# variant): tools/micro/read_bw.hip, profiles/r02_micro/read_bw.log
+HBM_READ_MEASURED_GBS = 6762.0
 GIB = float(1 << 30)
 SHARD_SEED = 0xC0FFEE
 
@@ -374,6 +377,8 @@ def roofline(kern_ms, local_bytes, K, config, world):
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+        "read_ceiling_measured": HBM_READ_MEASURED_GBS,
+        "frac_of_read_ceiling": round(achieved / HBM_READ_MEASURED_GBS, 4) if achieved else None,
         "traffic": traffic,
         "traffic_source": src,
         "algorithmic_bytes_per_launch": int(algo),
