@@ -107,7 +107,12 @@ def test_gpu_hollanti_golden_end_to_end(ci):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,efs,nq", [(10, 64, 1), (12, 1024, 3), (13, 100, 16), (16, 256, 2),
-                                      (14, 8, 5), (18, 1056, 4)])
+                                      (14, 8, 5), (18, 1056, 4),
+                                      # k_scan_uni shapes: VEC 4 -> 2 fallback (512 B, 3 rounds),
+                                      # several column groups (2 KiB, 1040 B), plane-table rounds
+                                      # 6-8, VEC 1 for 9-16, a 1-row range
+                                      (11, 512, 3), (11, 2048, 3), (12, 1040, 2), (11, 1024, 7),
+                                      (10, 1024, 8), (9, 2048, 12), (13, 4096, 1), (7, 1024, 3)])
 def test_gpu_answer_coefs_vs_oracle(n, efs, nq):
     import erasurecodedpir_amd as pir
     rng = np.random.default_rng(n * 131 + nq)
@@ -119,8 +124,10 @@ def test_gpu_answer_coefs_vs_oracle(n, efs, nq):
         lo, hi = (1 << n) // 3, (1 << n) - 7
         part = e.answer_coefs(coefs, lo, hi - lo)
         empty = e.answer_coefs(coefs, 5, 0)
+        one = e.answer_coefs(coefs, 77, 1)
     assert np.array_equal(full, O.scan(coefs, shard, efs))
     assert np.array_equal(part, O.scan(coefs, shard, efs, lo, hi))
+    assert np.array_equal(one, O.scan(coefs, shard, efs, 77, 78))
     assert not empty.any()
 
 

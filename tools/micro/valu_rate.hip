@@ -4,6 +4,8 @@
 //   MODE 1: v_bitop3_b32 z, z, x, m   (3 VGPR sources)
 //   MODE 2: v_xor_b32 z, x, z         (2 VGPR sources)
 //   MODE 3: v_xor_b32 z, s, z         (1 VGPR + 1 SGPR)
+//   MODE 4: v_perm_b32 z, z, x, m     (3 VGPR sources: a byte-table lookup)
+//   MODE 5: v_perm_b32 z, s, z, x     (SGPR table half + 2 VGPRs)
 // Reports lane-ops/s chip-wide and the shader clock from s_memtime over the same interval.
 // Build: hipcc -O3 --offload-arch=gfx950 -o valu_rate valu_rate.hip
 #include <hip/hip_runtime.h>
@@ -25,7 +27,9 @@ __global__ __launch_bounds__(1024) void k(uint32_t* out, uint32_t seed, int iter
       if constexpr (MODE == 0) z[i] = __builtin_amdgcn_bitop3_b32(z[i], x, s, 0x78);
       else if constexpr (MODE == 1) z[i] = __builtin_amdgcn_bitop3_b32(z[i], x, m, 0x78);
       else if constexpr (MODE == 2) z[i] ^= x;
-      else z[i] ^= s;
+      else if constexpr (MODE == 3) z[i] ^= s;
+      else if constexpr (MODE == 4) z[i] = __builtin_amdgcn_perm(z[i], x, m);
+      else z[i] = __builtin_amdgcn_perm(s, z[i], x);
     }
     asm volatile("" ::: "memory");
   }
@@ -68,6 +72,8 @@ int main() {
   run<1>(out, clk, cus);
   run<2>(out, clk, cus);
   run<3>(out, clk, cus);
+  run<4>(out, clk, cus);
+  run<5>(out, clk, cus);
   run<0>(out, clk, cus);
   return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
