@@ -444,7 +444,8 @@ __device__ __forceinline__ uint4 load_coef(const uint8_t* c, uint64_t i) {
   }
 }
 
-// z ^ (x & m) in one v_bitop3 (m an all-ones / all-zeros mask, wave-uniform in an SGPR)
+// z ^ (x & m) in one v_bitop3 (m an all-ones / all-zeros mask: wave-uniform in an SGPR, or a
+// per-lane VGPR -- left to itself the compiler emits v_and + v_xor for the per-lane form)
 __device__ __forceinline__ uint32_t mxor(uint32_t z, uint32_t x, uint32_t m) {
   return __builtin_amdgcn_bitop3_b32(z, x, m, 0x78);
 }
@@ -609,7 +610,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
         for (int k = 0; k < 8; ++k) {
           const uint32_t m = 0u - ((ca >> k) & 1u);
 #pragma unroll
-          for (int v = 0; v < VEC; ++v) Z[a][k][v] ^= x[u].v[v] & m;
+          for (int v = 0; v < VEC; ++v) Z[a][k][v] = mxor(Z[a][k][v], x[u].v[v], m);
         }
       }
   }
@@ -628,7 +629,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
       for (int k = 0; k < 8; ++k) {
         const uint32_t m = 0u - ((ca >> k) & 1u);
 #pragma unroll
-        for (int v = 0; v < VEC; ++v) Z[a][k][v] ^= x.v[v] & m;
+        for (int v = 0; v < VEC; ++v) Z[a][k][v] = mxor(Z[a][k][v], x.v[v], m);
       }
     }
   }
@@ -1010,7 +1011,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
                 for (int kk = 0; kk < 8; ++kk) {
                   const uint32_t m = 0u - ((ca >> kk) & 1u);
 #pragma unroll
-                  for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= x[u].v[v] & m;
+                  for (int v = 0; v < VEC; ++v) Z[a][kk][v] = mxor(Z[a][kk][v], x[u].v[v], m);
                 }
               }
             }
@@ -1501,7 +1502,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
           for (int kk = 0; kk < 8; ++kk) {
             const uint32_t m = 0u - ((ca >> kk) & 1u);
 #pragma unroll
-            for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= xr.v[v] & m;
+            for (int v = 0; v < VEC; ++v) Z[a][kk][v] = mxor(Z[a][kk][v], xr.v[v], m);
           }
         }
       }
