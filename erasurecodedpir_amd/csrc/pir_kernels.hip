@@ -538,6 +538,40 @@ __device__ __forceinline__ void planes_fold2(uint32_t (&Z)[8][2], uint32_t x0, u
 #undef PIR_FOLD2_Z
 #undef PIR_FOLD2_IN
 
+// the same for one dword per lane (records of one wave row at VEC = 1): 8 v_bitop3 per round
+#define PIR_FOLD1_BODY                            \
+  "v_bitop3_b32 %0, %0, %9, %10 bitop3:0x78\n\t" \
+  "v_bitop3_b32 %1, %1, %9, %11 bitop3:0x78\n\t" \
+  "v_bitop3_b32 %2, %2, %9, %12 bitop3:0x78\n\t" \
+  "v_bitop3_b32 %3, %3, %9, %13 bitop3:0x78\n\t" \
+  "v_bitop3_b32 %4, %4, %9, %14 bitop3:0x78\n\t" \
+  "v_bitop3_b32 %5, %5, %9, %15 bitop3:0x78\n\t" \
+  "v_bitop3_b32 %6, %6, %9, %16 bitop3:0x78\n\t" \
+  "v_bitop3_b32 %7, %7, %9, %17 bitop3:0x78"
+#define PIR_FOLD1_Z                                                                       \
+  "+v"(Z[0][0]), "+v"(Z[1][0]), "+v"(Z[2][0]), "+v"(Z[3][0]), "+v"(Z[4][0]), "+v"(Z[5][0]), \
+      "+v"(Z[6][0]), "+v"(Z[7][0])
+#define PIR_FOLD1_IN                                                                        \
+  "v"(x0), "s"(m[0]), "s"(m[1]), "s"(m[2]), "s"(m[3]), "s"(m[4]), "s"(m[5]), "s"(m[6]), "s"(m[7])
+
+__device__ __forceinline__ u32x8 planes_fold1_next(uint32_t (&Z)[8][1], uint32_t x0, const u32x8& m,
+                                                   uint32_t cn) {
+  u32x8 nx;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\t"
+               "s_load_dwordx8 %8, %18, %19\n\t" PIR_FOLD1_BODY
+               : PIR_FOLD1_Z, "=&s"(nx)
+               : PIR_FOLD1_IN, "s"(c_planes.m), "s"(cn << 5));
+  return nx;
+}
+__device__ __forceinline__ void planes_fold1(uint32_t (&Z)[8][1], uint32_t x0, const u32x8& m) {
+  uint32_t pad;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\t" PIR_FOLD1_BODY : PIR_FOLD1_Z, "=s"(pad) : PIR_FOLD1_IN);
+  (void)pad;
+}
+#undef PIR_FOLD1_BODY
+#undef PIR_FOLD1_Z
+#undef PIR_FOLD1_IN
+
 __device__ __forceinline__ uint32_t coef_byte(const uint4& c, int a) {
   const uint32_t w = a < 4 ? c.x : (a < 8 ? c.y : (a < 12 ? c.z : c.w));
   return (w >> (8 * (a & 3))) & 0xffu;
@@ -663,8 +697,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
 //   VEC = 4 (NQ <= 3) or NQ <= 2 : scalar branches on the coefficient bits (~4 v_xor of two
 //             VGPRs per dword instead of 8 v_bitop3 with an SGPR mask, which issue at 2/3 the
 //             rate: profiles/r02_micro/valu_rate.log),
-//   VEC = 2, NQ >= 3 : the 8 plane masks from the table (s_load_dwordx8, one round ahead),
-//   else    : SGPR masks (v_bitop3).
+//   VEC <= 2, NQ >= 3 : the 8 plane masks from the table (s_load_dwordx8, one round ahead;
+//             per-bit s_bfe masks held the 8-round batched scan to 1.5 TB/s on the scalar unit).
 // Wave w folds rows [w * nrec / nwaves, (w + 1) * nrec / nwaves) of its column group.
 template <int NQ, int NRP, int VEC>
 __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(kScanThreads / 64 * kScanBlocksPerCU / 4)))
@@ -676,7 +710,7 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
   constexpr int GW = kColGroupLanes * VEC;
   constexpr int U = NQ <= 2 ? 8 : 4;  // divides 64 (the coefficient block)
   constexpr bool kBranch = VEC == 4 || NQ <= 2;
-  constexpr bool kAsm = !kBranch && VEC == 2 && NQ >= 3;
+  constexpr bool kAsm = !kBranch && VEC <= 2 && NQ >= 3;
   __shared__ uint32_t red[NQ * GW];
   for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) red[i] = 0;
 
@@ -727,9 +761,15 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
               u32x8 m = plane_masks_issue(coef_byte(cf, 0));
 #pragma unroll
               for (int a = 0; a < NQ; ++a) {
-                auto& Za = reinterpret_cast<uint32_t(&)[8][2]>(Z[a]);
-                if (a + 1 < NQ) m = planes_fold2_next(Za, x[u].v[0], x[u].v[1], m, coef_byte(cf, a + 1));
-                else planes_fold2(Za, x[u].v[0], x[u].v[1], m);
+                if constexpr (VEC == 2) {
+                  auto& Za = reinterpret_cast<uint32_t(&)[8][2]>(Z[a]);
+                  if (a + 1 < NQ) m = planes_fold2_next(Za, x[u].v[0], x[u].v[1], m, coef_byte(cf, a + 1));
+                  else planes_fold2(Za, x[u].v[0], x[u].v[1], m);
+                } else {
+                  auto& Za = reinterpret_cast<uint32_t(&)[8][1]>(Z[a]);
+                  if (a + 1 < NQ) m = planes_fold1_next(Za, x[u].v[0], m, coef_byte(cf, a + 1));
+                  else planes_fold1(Za, x[u].v[0], m);
+                }
               }
             } else {
 #pragma unroll
