@@ -6,6 +6,11 @@
 //   MODE 3: v_xor_b32 z, s, z         (1 VGPR + 1 SGPR)
 //   MODE 4: v_perm_b32 z, z, x, m     (3 VGPR sources: a byte-table lookup)
 //   MODE 5: v_perm_b32 z, s, z, x     (SGPR table half + 2 VGPRs)
+//   MODE 6: v_and_or_b32 z, z, x, m   MODE 7: v_lshl_or_b32 z, z, 8, x   MODE 8: v_bfe_u32 z, z, 8, 8
+//   MODE 9: v_alignbit_b32 z, z, x, 8 MODE 10: v_add_u32 z, z, x          MODE 11: v_bfi_b32 z, x, z, m
+//   MODE 12: v_lshrrev_b32 z, 8, z    MODE 13: v_and_b32 z, z, x
+//   MODE 14: v_mov_b32_sdwa z, x dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2
+//   MODE 15: v_or_b32_sdwa z, z, x src1_sel:BYTE_3
 // Reports lane-ops/s chip-wide and the shader clock from s_memtime over the same interval.
 // Build: hipcc -O3 --offload-arch=gfx950 -o valu_rate valu_rate.hip
 #include <hip/hip_runtime.h>
@@ -29,7 +34,18 @@ __global__ __launch_bounds__(1024) void k(uint32_t* out, uint32_t seed, int iter
       else if constexpr (MODE == 2) z[i] ^= x;
       else if constexpr (MODE == 3) z[i] ^= s;
       else if constexpr (MODE == 4) z[i] = __builtin_amdgcn_perm(z[i], x, m);
-      else z[i] = __builtin_amdgcn_perm(s, z[i], x);
+      else if constexpr (MODE == 5) z[i] = __builtin_amdgcn_perm(s, z[i], x);
+      else if constexpr (MODE == 6) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(z[i]) : "v"(x), "v"(m));
+      else if constexpr (MODE == 7) asm volatile("v_lshl_or_b32 %0, %0, 8, %1" : "+v"(z[i]) : "v"(x));
+      else if constexpr (MODE == 8) asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(z[i]));
+      else if constexpr (MODE == 9) asm volatile("v_alignbit_b32 %0, %0, %1, 8" : "+v"(z[i]) : "v"(x));
+      else if constexpr (MODE == 10) asm volatile("v_add_u32_e32 %0, %1, %0" : "+v"(z[i]) : "v"(x));
+      else if constexpr (MODE == 11) asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(z[i]) : "v"(x), "v"(m));
+      else if constexpr (MODE == 12) asm volatile("v_lshrrev_b32_e32 %0, 8, %0" : "+v"(z[i]));
+      else if constexpr (MODE == 13) asm volatile("v_and_b32_e32 %0, %1, %0" : "+v"(z[i]) : "v"(x));
+      else if constexpr (MODE == 14)
+        asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(z[i]) : "v"(x));
+      else asm volatile("v_or_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "+v"(z[i]) : "v"(x));
     }
     asm volatile("" ::: "memory");
   }
@@ -74,6 +90,16 @@ int main() {
   run<3>(out, clk, cus);
   run<4>(out, clk, cus);
   run<5>(out, clk, cus);
+  run<6>(out, clk, cus);
+  run<7>(out, clk, cus);
+  run<8>(out, clk, cus);
+  run<9>(out, clk, cus);
+  run<10>(out, clk, cus);
+  run<11>(out, clk, cus);
+  run<12>(out, clk, cus);
+  run<13>(out, clk, cus);
+  run<14>(out, clk, cus);
+  run<15>(out, clk, cus);
   run<0>(out, clk, cus);
   return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
