@@ -115,6 +115,7 @@ struct pir_engine {
   int batch_group = 0;          // keys per shard pass (0: automatic; $PIR_BATCH_G)
   int last_batch_group = 0;
   int batch_scan_bpc = 2;       // scan workgroups per CU in batched answers ($PIR_BATCH_SCAN_BPC)
+  int batch_k_last = -1;        // levels of the batched leaf stage (-1: make_plan's; $PIR_BATCH_KLAST)
   uint8_t* d_result = nullptr;  // nq*efs (host-API staging)
   uint8_t* d_qscratch = nullptr;  // k_query super-tile tile inputs
   size_t qscratch_cap = 0;
@@ -372,7 +373,7 @@ int answer_batch_core(pir_engine* e, const uint8_t* d_raw, int nk, int log_parts
   e->last_batch_group = G;
   e->last_fused = 0;
   e->last_chunks = 1;
-  const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix);
+  const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix, e->batch_k_last);
   const pir::ScanShape sh =
       pir::make_scan_shape(pl.nleaves, e->pitch, W, e->num_cus, e->batch_scan_bpc);
   const size_t cb_bytes = (size_t)pl.nleaves * W;
@@ -753,6 +754,8 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
     if (bg) e->batch_group = atoi(bg);
     const char* bb = getenv("PIR_BATCH_SCAN_BPC");
     if (bb) e->batch_scan_bpc = std::max(1, atoi(bb));
+    const char* bk = getenv("PIR_BATCH_KLAST");
+    if (bk) e->batch_k_last = std::max(1, std::min(12, atoi(bk)));
     const int tile = pir::fused_tile(c.num_rounds, e->pitch, e->rows, e->num_cus);
     if (tile) {
       const pir::TreePlan pf =
