@@ -208,3 +208,25 @@ def test_gpu_mp_full_size():
     for a in range(nrk):
         want[a] = np.bitwise_xor.reduce(gf[share[a][:, None], recs.reshape(mu, efs)], axis=0)
     assert np.array_equal(one, want)
+
+
+@pytest.mark.gpu
+def test_gpu_mp_and_coefs_through_the_exchange():
+    """The split-shard exchange (ncclAllGather + XOR fold) on the multiparty and explicit-
+    coefficient answers, with a 1-rank communicator: equal to the no-communicator answers."""
+    import erasurecodedpir_amd as pir
+    p, t, n, efs = 3, 1, 14, 96
+    nrk = pir.mp_num_keys(p, t)
+    key = O.mp_key(p, n, t, 99)
+    shard = O.xorshift(5, (1 << n) * efs)
+    coefs = np.random.default_rng(1).integers(0, 256, (nrk, 1 << n), dtype=np.uint8)
+    out = []
+    for comm in (False, True):
+        with pir.Engine(2, 1, n, efs, nrk) as e:
+            e.set_shard(shard)
+            if comm:
+                e.attach_comm(pir.comm_unique_id(), 1, 0)
+            out.append((e.answer_mp(key, p, t), e.answer_mp(key, p, t, 1, 4), e.answer_coefs(coefs)))
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    assert np.array_equal(out[0][0], O.mp_answer(p, t, n, efs, key, shard))
