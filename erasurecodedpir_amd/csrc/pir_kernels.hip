@@ -2004,6 +2004,10 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
   // tile is built during the scan of the previous one, and wide tiles spend a smaller share of
   // their tree in latency-bound narrow levels (a lone query keeps 1024: shorter first tile)
   if (nk > 1 && nq <= 2 && nleaves >= (uint64_t)4096 * 256) tile = 4096;
+  if (const char* tq = getenv("PIR_QUERY_TILEQ")) {  // diagnostics: a queue's tile size
+    const int t = atoi(tq);
+    if (nk > 1 && (t == 1024 || (t == 4096 && nq <= 2 && nleaves >= (uint64_t)4096 * 256))) tile = t;
+  }
   // a lone query of large records waits for its first tile before any row is scanned: smaller
   // tiles (fewer, cheaper levels under a deeper root) start the scan sooner ($PIR_QUERY_TILE1)
   if (nk == 1 && nq <= 2 && pitch > 256 && tile == 1024) {
