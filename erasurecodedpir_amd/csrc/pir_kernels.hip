@@ -2013,7 +2013,8 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
   if (nk == 1 && nq <= 2 && pitch > 256 && tile == 1024) {
     int t1 = kLoneTile;
     if (const char* tv = getenv("PIR_QUERY_TILE1")) t1 = atoi(tv);
-    if (t1 == 256 || t1 == 512 || t1 == 1024) tile = t1;
+    if (t1 == 256 || t1 == 512 || t1 == 1024 || (t1 == 4096 && nleaves >= (uint64_t)4096 * 256))
+      tile = t1;
   }
   // records of <= 256 B: a tile's rows stream in a quarter of the time its tree takes, so 12 of
   // the 16 waves build trees and 4 scan ($PIR_QUERY_TW = 8 or 12 overrides)
@@ -2037,9 +2038,12 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
   // query of large records waits for its first tile, and a super-tile's top is wider than one
   // tile's.
   qp.ls = std::min(qp.lt, kt - 1 - kQueryKin);
+  const int ls_max = qp.ls;
   if (nk == 1 && !(nq <= 2 && pitch <= 256)) qp.ls = 0;
-  if (const char* sv = getenv("PIR_QUERY_SUPER"))
+  if (const char* sv = getenv("PIR_QUERY_SUPER")) {
     if (sv[0] == '0') qp.ls = 0;
+    if (sv[0] == '1') qp.ls = ls_max;
+  }
   qp.shape = make_fused_shape(nleaves, pitch, nq, num_cus, tile);
   qp.shape.grid.x = 1u << lr;
   return qp;
