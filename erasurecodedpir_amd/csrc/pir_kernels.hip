@@ -472,6 +472,10 @@ typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 // k_query: rounds up to which the scan waves fold with scalar branches instead of plane-table
 // masks.  Branches measured slower at 5 rounds (c5: 8.36 vs 6.34 ms per query; the k_query scan
 // waves are too few per SIMD to hide the scalar issue), so only 1-2 rounds take them.
+// k_query scan waves' issue priority over the tree waves (s_setprio)
+#ifndef PIR_SCAN_PRIO
+#define PIR_SCAN_PRIO 2
+#endif
 #ifndef PIR_QUERY_BRANCH_MAXNQ
 #define PIR_QUERY_BRANCH_MAXNQ 2
 #endif
@@ -1503,7 +1507,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
     // past the tile's row groups are masked)
     const uint32_t rpt = ((ngroups + nwg - 1) / nwg + U - 1) / U * U;
     const bool scan = wi < nwg && !(trace && trace_flags_noscan);
-    __builtin_amdgcn_s_setprio(2);
+    __builtin_amdgcn_s_setprio(PIR_SCAN_PRIO);
     const uint8_t* rbase = shard + (b * region_rows) * pitch + (uint64_t)chunk * CH;
     // Rolling load pipeline: x[u] holds slot j0 + u; once it is folded, slot j0 + U + u is loaded
     // into it -- at the end of a tile, from the next tile (of this or the next query).  Shard rows
