@@ -69,15 +69,19 @@ __device__ __forceinline__ void load_tables(uint32_t* lds) {
 // and entry (i >> 6) is wave-uniform, so the loads are scalar
 template <int NT>
 __device__ __forceinline__ void load_tables_n(uint32_t* lds) {
-  constexpr int K = 256 * 64 / NT;
+  constexpr int K = (256 * 64 + NT - 1) / NT;  // NT a multiple of 64 (768 leaves a partial pass)
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t v[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) v[k] = c_te0[wv + k * (NT / 64)];
+  for (int k = 0; k < K; ++k) {
+    const uint32_t e = wv + k * (NT / 64);
+    v[k] = e < 256 ? c_te0[e] : 0u;
+  }
   const bool hi = threadIdx.x & 32;
 #pragma unroll
   for (int k = 0; k < K; ++k)
-    lds[threadIdx.x + k * NT] = hi ? __builtin_amdgcn_alignbit(v[k], v[k], 16) : v[k];
+    if ((256 * 64) % NT == 0 || wv + k * (NT / 64) < 256)
+      lds[threadIdx.x + k * NT] = hi ? __builtin_amdgcn_alignbit(v[k], v[k], 16) : v[k];
 }
 
 // SubWord(RotWord(k3)) ^ rcon, then the word chain (FIPS-197 5.2)

@@ -113,6 +113,7 @@ struct QueryPlan {
   int tile, lr, lt;
   int ls;           // 2^ls tiles per super-tile (their narrow top levels expanded once)
   int tw;           // tree waves per workgroup (the rest scan)
+  int m4r;          // 4-5 rounds: the 768-thread four-Russians k_query (1: kM4rTW tree waves, 2: two)
   ScanShape shape;  // grid.x = 2^lr workgroups (slabs), grid.y = column groups
 };
 QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, int num_cus,

@@ -16,6 +16,7 @@
 // HBM stream costs ~1 VALU op per byte.
 #include "pir_kernels.h"
 #include "pir_aes.h"
+#include "pir_m4r.h"
 
 #include <algorithm>
 #include <stdlib.h>
@@ -714,7 +715,10 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
   constexpr int GW = kColGroupLanes * VEC;
   constexpr int U = NQ <= 2 ? 8 : 4;  // divides 64 (the coefficient block)
   constexpr bool kBranch = VEC == 4 || NQ <= 2;
-  constexpr bool kAsm = !kBranch && VEC <= 2 && NQ >= 3;
+  // one dword per lane, 4-8 rounds: four Russians over groups of 4 rows (pir_m4r.h; 8 NQ + 16
+  // VGPRs of planes and row combinations fit the 128 of 16 waves per CU)
+  constexpr bool kM4R = VEC == 1 && NQ >= 4 && NQ <= 8 && NRP >= 4 && NRP <= 8;
+  constexpr bool kAsm = !kBranch && !kM4R && VEC <= 2 && NQ >= 3;
   __shared__ uint32_t red[NQ * GW];
   for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) red[i] = 0;
 
@@ -749,9 +753,31 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
 #pragma unroll
     for (int u = 0; u < U; ++u) load_row(r0 + u, x[u]);
     uint4 c4 = coefs64(r0);
+    // kM4R: lane 8a + b builds plane (a, b)'s index from bit b of the round-a coefficient bytes
+    const uint32_t m4r_sh = 8u * ((lane >> 3) & 3u) + (lane & 7u);
+    const bool m4r_hi = lane >= 32;
     for (uint64_t rb = r0; rb < r1; rb += 64) {
       const uint4 c4n = coefs64(rb + 64);  // the next 64 rows' coefficients, in flight
       const uint32_t nb = (uint32_t)(r1 - rb < 64 ? r1 - rb : 64);
+      if constexpr (kM4R) {
+        // groups of 4 rows; rows past the wave's last have zero coefficients (no plane takes
+        // them) and re-read its first row
+        for (uint32_t j0 = 0; j0 < nb; j0 += 4) {
+          uint32_t vi = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t w = m4r_hi ? __builtin_amdgcn_readlane(c4.y, j0 + r)
+                                      : __builtin_amdgcn_readlane(c4.x, j0 + r);
+            vi |= ((w >> m4r_sh) & 1u) << r;
+          }
+          m4r_fold4<VEC, NQ>(Z, x[0].v, x[1].v, x[2].v, x[3].v, vi);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) load_row(rb + j0 + r + U, x[r]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        c4 = c4n;
+        continue;
+      }
       for (uint32_t j0 = 0; j0 < nb; j0 += U) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -841,6 +867,8 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
 // ------------------------------------------------------------------------------------------
 constexpr int kFusedThreads = 1024;
 constexpr int kFusedWaves = kFusedThreads / 64;
+constexpr int kM4rThreads = 768;  // k_query, 4-5 rounds: 4 tree + 8 scan waves, 168 VGPRs each
+constexpr int kM4rTW = 4;
 
 template <int TILE, int NRP, int NQ, int VEC, int GYMAX>
 struct FusedSmem {
@@ -1152,8 +1180,9 @@ __device__ __forceinline__ void stage_key(const uint8_t* __restrict__ raw, int p
   }
 }
 
-template <int NQ, int NRP, int VEC, bool UNI, int TW, int TILE, int GYMAX, int RING>
-__global__ __launch_bounds__(kFusedThreads) void k_query(
+template <int NQ, int NRP, int VEC, bool UNI, int TW, int TILE, int GYMAX, int RING,
+          int NT = kFusedThreads>
+__global__ __launch_bounds__(NT) void k_query(
     const uint8_t* __restrict__ raw0, uint32_t key_stride, int nk, int p, int n, int nq,
     int party0, int log_parts, uint64_t prefix, int lr, int lt, int ls,
     uint4* __restrict__ fr_s, uint32_t* __restrict__ fr_t, const uint8_t* __restrict__ shard,
@@ -1169,7 +1198,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
   const bool trace_flags_noscan = trace && (trace[(uint64_t)kQueryTraceSlots * gridDim.x] & 1u);
   if (trace) trace += (uint64_t)blockIdx.x * kQueryTraceSlots;
   if (trace && threadIdx.x == 0) { trace[0] = wall_clock64(); trace[56] = clock64(); }
-  constexpr int SW = kFusedWaves - TW;
+  constexpr int NWV = NT / 64;  // waves per workgroup
+  constexpr int SW = NWV - TW;
   constexpr int CH = VEC * 4;
   constexpr int GW = kColGroupLanes * VEC;
   constexpr int KT = TILE == 4096 ? 12 : (TILE == 1024 ? 10 : (TILE == 512 ? 9 : 8));  // log2 TILE
@@ -1178,9 +1208,9 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
   static_assert(sizeof(Smem) <= 160 * 1024, "LDS");
   __shared__ Smem sm;
   const uint32_t pm1 = (uint32_t)p - 1;
-  load_tables_n<kFusedThreads>(sm.tab);
+  load_tables_n<NT>(sm.tab);
   for (int i = threadIdx.x; i < GYMAX * NQ * GW; i += blockDim.x) (&sm.red[0][0])[i] = 0;
-  stage_key(raw0, p, n, nq, threadIdx.x, kFusedThreads, sm.scw, sm.tcw, sm.lastcw);
+  stage_key(raw0, p, n, nq, threadIdx.x, NT, sm.scw, sm.tcw, sm.lastcw);
   if (threadIdx.x == 0) {
     sm.bar = 0; sm.sbar = 0; sm.ready = 0;
     for (int r = 0; r < RING; ++r) sm.consumed[r] = 0;
@@ -1233,7 +1263,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
     // the whole workgroup: hardware barrier (waiting waves sleep); the tree waves alone: LDS
     // counter barrier (the scan waves keep streaming)
     auto sync = [&]() __attribute__((always_inline)) {
-      if (team == (uint32_t)kFusedWaves) __syncthreads();
+      if (team == (uint32_t)NWV) __syncthreads();
       else group_barrier(&sm.bar, gen, team);
     };
     if (i == 0 && g > 0) {  // next query: its key replaces the previous one's (all tree waves
@@ -1403,7 +1433,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
     {
       const uint4* is = buf ? sm.sb : sm.sa;
       const uint32_t* it = buf ? sm.tb : sm.ta;
-      if (team == (uint32_t)kFusedWaves) {  // 3 lanes per parent; the child lanes convert
+      if (team == (uint32_t)NWV) {  // 3 lanes per parent; the child lanes convert
         const int l = tt & 63, ul = l / 3, r = l - 3 * ul;
         const int npp = (nt >> 6) * 21;
         const int u0 = (tt >> 6) * 21 + ul;
@@ -1460,7 +1490,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
     if (trace && tt == 0 && g < 32) { trace[64 + g] = wall_clock64(); trace[128 + g] = clock64(); }
   };
 
-  tree_tile(0, kFusedThreads, kFusedWaves);  // every wave builds the first tile
+  tree_tile(0, NT, NWV);  // every wave builds the first tile
   if (wave < (uint32_t)TW) {
     // ===================================== tree role ======================================
     for (uint32_t g = 1; g < total; ++g) {
@@ -1499,10 +1529,17 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
     // many rounds, wave-uniform coefficients, 2 dwords per lane: scalar branches on the
     // coefficient bits (avg 4 two-VGPR v_xor per dword and round) up to PIR_QUERY_BRANCH_MAXNQ
     // rounds, else masks from the plane table (8 v_bitop3 with an SGPR mask, 2/3 the issue rate)
-    constexpr bool kPlaneAsm = UNI && VEC == 2 && NQ >= 3 && NQ > PIR_QUERY_BRANCH_MAXNQ;
+    // 768-thread workgroups (4 to 5 rounds): four Russians over groups of 4 rows (pir_m4r.h:
+    // 2.5x fewer VALU ops than the masks, 32 more VGPRs -- which 16 waves per CU do not have)
+    constexpr bool kM4R = UNI && VEC == 2 && NQ >= 4 && NQ <= 5 && NT == kM4rThreads;
+    constexpr bool kPlaneAsm = !kM4R && UNI && VEC == 2 && NQ >= 3 && NQ > PIR_QUERY_BRANCH_MAXNQ;
     // rows in flight per lane (one record per wave row: a rolling pipeline whose x[] stays live
     // across tiles; several records per row: U rows loaded, then folded, per batch)
-    constexpr int U = kPlaneAsm ? PIR_PLANE_U : (SW >= 8 ? 8 : 16);
+    constexpr int U = (kPlaneAsm || kM4R) ? PIR_PLANE_U : (SW >= 8 ? 8 : 16);
+    static_assert(!kM4R || U % 4 == 0, "four Russians: groups of 4 rows");
+    // kM4R: lane 8a + b builds plane (a, b)'s index from bit b of the round-a coefficient bytes
+    const uint32_t m4r_sh = 8u * ((lane >> 3) & 3u) + (lane & 7u);
+    const bool m4r_hi = lane >= 32;
     // row slot j of a tile = row group wi + j * nwg; rpt slots per tile, a multiple of U (slots
     // past the tile's row groups are masked)
     const uint32_t rpt = ((ngroups + nwg - 1) / nwg + U - 1) / U * U;
@@ -1588,6 +1625,23 @@ __global__ __launch_bounds__(kFusedThreads) void k_query(
           if (gl >= ngroups) c4 = make_uint4(0, 0, 0, 0);
           const bool last = j0 + U == rpt;
           const uint32_t gn = last ? g + 1 : g, jn = last ? 0u : j0 + U;
+          if constexpr (kM4R) {
+#pragma unroll
+            for (int g4 = 0; g4 < U; g4 += 4) {
+              uint32_t vi = 0;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const uint32_t w = m4r_hi ? __builtin_amdgcn_readlane(c4.y, g4 + r)
+                                          : __builtin_amdgcn_readlane(c4.x, g4 + r);
+                vi |= ((w >> m4r_sh) & 1u) << r;
+              }
+              m4r_fold4<VEC, NQ>(Z, x[g4].v, x[g4 + 1].v, x[g4 + 2].v, x[g4 + 3].v, vi);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) load_slot(gn, jn + g4 + r, x[g4 + r]);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+            continue;
+          }
           u32x8 mrow;  // kPlaneAsm: masks of the next row's round 0, in flight
           if constexpr (kPlaneAsm) mrow = plane_masks_issue(__builtin_amdgcn_readlane(c4.x, 0) & 0xffu);
 #pragma unroll
@@ -2027,6 +2081,13 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
     const int v = atoi(tw);
     if (v == kFusedTW || (v == kQueryTreeHeavyTW && nq <= 2)) qp.tw = v;
   }
+  // 4-5 rounds at VEC 2 with one record per wave row: the four-Russians k_query (768 threads:
+  // 4 tree + 8 scan waves) unless $PIR_QUERY_M4R=0
+  qp.m4r = nq >= 4 && nq <= 5 && nq > PIR_QUERY_BRANCH_MAXNQ && tile == 1024 &&
+           pitch / 8 >= (uint32_t)kColGroupLanes;
+  if (const char* mv = getenv("PIR_QUERY_M4R")) qp.m4r = qp.m4r && atoi(mv) != 0;
+  // diagnostics: $PIR_QUERY_M4R_TW=2 -> 2 tree + 10 scan waves (default 4 + 8)
+  if (const char* mt = getenv("PIR_QUERY_M4R_TW")) qp.m4r = qp.m4r ? (atoi(mt) == 2 ? 2 : 1) : 0;
   int kt = 0;
   while ((1 << kt) < tile) ++kt;
   int lr = 0;
@@ -2064,11 +2125,19 @@ static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t k
   constexpr int VEC = NQ <= 2 ? 4 : 2;
   constexpr int RING = TILE == 4096 ? 2 : 4;  // share slots: the tree runs RING-1 tiles ahead
   const ScanShape& sh = qp.shape;
-#define PIR_QL(UNI, TW, GY, gy)                                                                  \
-  hipLaunchKernelGGL((k_query<NQ, NRP, VEC, UNI, TW, TILE, GY, RING>), dim3(sh.grid.x),          \
-                     dim3(kFusedThreads), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,          \
+#define PIR_QLN(UNI, TW, GY, gy, NTH)                                                            \
+  hipLaunchKernelGGL((k_query<NQ, NRP, VEC, UNI, TW, TILE, GY, RING, NTH>), dim3(sh.grid.x),     \
+                     dim3(NTH), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,                    \
                      log_parts, prefix, qp.lr, qp.lt, qp.ls, fr_s, fr_t, shard, sh.pitch, sh.cpr,  \
                      gy, slabs, trace, out, qcnt, efs)
+#define PIR_QL(UNI, TW, GY, gy) PIR_QLN(UNI, TW, GY, gy, kFusedThreads)
+  if constexpr (VEC == 2 && NQ >= 4 && NQ <= 5 && NQ > PIR_QUERY_BRANCH_MAXNQ && TILE == 1024) {
+    if (sh.uniform && qp.m4r) {  // four-Russians scan waves (k_query's kM4R)
+      if (qp.m4r == 2) PIR_QLN(true, 2, 4, sh.grid.y, kM4rThreads);  // diagnostics: 2 tree waves
+      else PIR_QLN(true, kM4rTW, 4, sh.grid.y, kM4rThreads);
+      return hipGetLastError();
+    }
+  }
   if constexpr (NQ <= 2) {
     if (qp.tw == kQueryTreeHeavyTW) {  // small records: the tree is the bottleneck
       if (sh.uniform) PIR_QL(true, kQueryTreeHeavyTW, 4, sh.grid.y);
@@ -2079,6 +2148,7 @@ static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t k
   if (sh.uniform) PIR_QL(true, kFusedTW, 4, sh.grid.y);
   else PIR_QL(false, kFusedTW, 1, 1u);
 #undef PIR_QL
+#undef PIR_QLN
   return hipGetLastError();
 }
 

@@ -112,7 +112,10 @@ def test_gpu_hollanti_golden_end_to_end(ci):
                                       # several column groups (2 KiB, 1040 B), plane-table rounds
                                       # 6-8, VEC 1 for 9-16, a 1-row range
                                       (11, 512, 3), (11, 2048, 3), (12, 1040, 2), (11, 1024, 7),
-                                      (10, 1024, 8), (9, 2048, 12), (13, 4096, 1), (7, 1024, 3)])
+                                      (10, 1024, 8), (9, 2048, 12), (13, 4096, 1), (7, 1024, 3),
+                                      # one dword per lane, 4-8 rounds: four-Russians folds
+                                      (12, 256, 5), (11, 300, 8), (12, 400, 4), (10, 256, 6),
+                                      (7, 256, 7)])
 def test_gpu_answer_coefs_vs_oracle(n, efs, nq):
     import erasurecodedpir_amd as pir
     rng = np.random.default_rng(n * 131 + nq)

@@ -166,7 +166,7 @@ static int run(const char* name, const uint8_t* shard, uint64_t nrec, const uint
 int main() {
   int cus;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  const uint64_t nrec = 1ull << 22;  // 4 GiB; rows per wave a multiple of 8 for every variant
+  const uint64_t nrec = 3ull << 20;  // 3 GiB; rows per wave a multiple of 8 for every variant
   uint8_t* shard;
   uint2* coef;
   u32x8* mtab;
