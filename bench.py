@@ -69,6 +69,7 @@ CONFIGS = {
 COEF_CONFIGS = {
     "ch": (24, 1024, 1, "polynomial (Hollanti) PIR: 2^24 x 1 KiB shard, 1 round, explicit coefficient vector"),
     "ch3": (24, 1024, 3, "polynomial (Hollanti) PIR: 2^24 x 1 KiB shard, 3 rounds (k=3), explicit coefficient vectors"),
+    "ch5": (24, 1024, 5, "polynomial (Hollanti) PIR: 2^24 x 1 KiB shard, 5 rounds (k=5), explicit coefficient vectors"),
 }
 # multiparty sqrt(N) DPF answers: a step = one query's key (device-resident) evaluated into
 # NUM_RSS_KEYS shares and scanned against the shard (server.cpp:136-176)

@@ -90,7 +90,11 @@ struct ScanShape {
   uint32_t pitch, cpr;   // bytes per row, chunks per row
   uint32_t slab_bytes;   // per-workgroup partial = nq * 64 * vec * 4
   dim3 grid;
+  int threads;           // k_scan_uni workgroup: kScanThreads, or kScanM4rThreads (4-5 rounds)
 };
+// k_scan_uni for 4-5 rounds at two dwords per lane: four-Russians folds need 168 VGPRs, so one
+// 768-thread workgroup per CU (only where the caller leaves the CU to the scan: blocks_per_cu 0)
+constexpr int kScanM4rThreads = 768;
 // blocks_per_cu <= 0: kScanBlocksPerCU.  One block per CU leaves room on every CU for a
 // 1024-thread tree workgroup beside the scan (batched answers overlap the two).
 ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus, int blocks_per_cu = 0);

@@ -705,8 +705,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
 //   VEC <= 2, NQ >= 3 : the 8 plane masks from the table (s_load_dwordx8, one round ahead;
 //             per-bit s_bfe masks held the 8-round batched scan to 1.5 TB/s on the scalar unit).
 // Wave w folds rows [w * nrec / nwaves, (w + 1) * nrec / nwaves) of its column group.
-template <int NQ, int NRP, int VEC>
-__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(kScanThreads / 64 * kScanBlocksPerCU / 4)))
+template <int NQ, int NRP, int VEC, int NT = kScanThreads>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kScanThreads ? kScanThreads / 64 * kScanBlocksPerCU / 4 : NT / 256)))
 void k_scan_uni(const uint8_t* __restrict__ shard,
                                                            uint64_t nrec, uint32_t pitch,
                                                            uint32_t cpr, const uint8_t* __restrict__ c,
@@ -715,9 +715,11 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
   constexpr int GW = kColGroupLanes * VEC;
   constexpr int U = NQ <= 2 ? 8 : 4;  // divides 64 (the coefficient block)
   constexpr bool kBranch = VEC == 4 || NQ <= 2;
-  // one dword per lane, 4-8 rounds: four Russians over groups of 4 rows (pir_m4r.h; 8 NQ + 16
-  // VGPRs of planes and row combinations fit the 128 of 16 waves per CU)
-  constexpr bool kM4R = VEC == 1 && NQ >= 4 && NQ <= 8 && NRP >= 4 && NRP <= 8;
+  // four Russians over groups of 4 rows (pir_m4r.h): one dword per lane for 4-8 rounds (8 NQ +
+  // 16 VGPRs of planes and row combinations fit the 128 of 16 waves per CU), two dwords for 4-5
+  // rounds in the 768-thread instance (16 NQ + 32 VGPRs: 168 per wave at 12 waves per CU)
+  constexpr bool kM4R = (VEC == 1 && NQ >= 4 && NQ <= 8 && NRP >= 4 && NRP <= 8) ||
+                        (VEC == 2 && NQ >= 4 && NQ <= 5 && NT == kScanM4rThreads);
   constexpr bool kAsm = !kBranch && !kM4R && VEC <= 2 && NQ >= 3;
   __shared__ uint32_t red[NQ * GW];
   for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) red[i] = 0;
@@ -2302,6 +2304,15 @@ ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus, in
   const uint64_t waves_per_block = kScanThreads / 64;
   uint64_t gx = std::max<uint64_t>(1, std::min<uint64_t>(want_blocks / gy, (groups + 4 * waves_per_block - 1) / (4 * waves_per_block)));
   sh.grid = dim3((unsigned)gx, gy);
+  sh.threads = kScanThreads;
+  if (blocks_per_cu <= 0 && sh.uniform && sh.vec == 2 && (nq == 4 || nq == 5) &&
+      !(getenv("PIR_SCAN_M4R") && atoi(getenv("PIR_SCAN_M4R")) == 0)) {
+    // the four-Russians k_scan_uni: one 768-thread workgroup per CU and column group
+    const uint64_t wpb = kScanM4rThreads / 64;
+    gx = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)num_cus / gy, (groups + 4 * wpb - 1) / (4 * wpb)));
+    sh.grid = dim3((unsigned)gx, gy);
+    sh.threads = kScanM4rThreads;
+  }
   sh.slab_bytes = (uint32_t)(nq * kColGroupLanes * sh.vec * 4);
   return sh;
 }
@@ -2320,6 +2331,14 @@ static hipError_t scan_nq(const ScanShape& sh, const uint8_t* d_shard, uint64_t 
     }
   }
   if (sh.vec != VEC) return hipErrorInvalidValue;
+  if constexpr (VEC == 2 && NQ >= 4 && NQ <= 5) {
+    if (sh.uniform && sh.threads == kScanM4rThreads) {
+      hipLaunchKernelGGL((k_scan_uni<NQ, NRP, VEC, kScanM4rThreads>), sh.grid,
+                         dim3(kScanM4rThreads), 0, s, d_shard, nrec, sh.pitch, sh.cpr, d_c,
+                         d_slabs, acc);
+      return hipGetLastError();
+    }
+  }
   if (sh.uniform)
     hipLaunchKernelGGL((k_scan_uni<NQ, NRP, VEC>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
                        nrec, sh.pitch, sh.cpr, d_c, d_slabs, acc);

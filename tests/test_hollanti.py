@@ -115,7 +115,9 @@ def test_gpu_hollanti_golden_end_to_end(ci):
                                       (10, 1024, 8), (9, 2048, 12), (13, 4096, 1), (7, 1024, 3),
                                       # one dword per lane, 4-8 rounds: four-Russians folds
                                       (12, 256, 5), (11, 300, 8), (12, 400, 4), (10, 256, 6),
-                                      (7, 256, 7)])
+                                      (7, 256, 7),
+                                      # two dwords per lane, 4-5 rounds: the 768-thread kernel
+                                      (12, 1024, 5), (11, 512, 4), (10, 2048, 5), (9, 1040, 5)])
 def test_gpu_answer_coefs_vs_oracle(n, efs, nq):
     import erasurecodedpir_amd as pir
     rng = np.random.default_rng(n * 131 + nq)
