@@ -32,3 +32,27 @@ def test_checker_flags_an_early_reader():
     assert n == 1 and len(bad) == 1 and "s_mov_b32" in bad[0][2]
     clean = asm.replace("s_mov_b32 s50, s37", "s_mov_b32 s50, s51")
     assert C.check(clean) == ([], 1)
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libpir_engine.so not built")
+def test_four_russians_index_windows_are_clean():
+    """Every GPR-index window of the four-Russians folds (csrc/pir_m4r.h) holds only the fold's
+    instructions, each index change has its wait state, and no spill lane sits in v96-v127."""
+    import check_m4r_asm as M
+    bad, n = M.check(M.disassemble(LIB))
+    assert n > 0, "no index windows: the four-Russians k_query / k_scan_uni instances are missing"
+    assert not bad, "\n".join(f"{f}: {p}" for f, p in bad)
+
+
+def test_four_russians_checker_flags_problems():
+    import check_m4r_asm as M
+    good = ["0000 <k>:", "\tv_readlane_b32 s6, v62, 0", "\ts_set_gpr_idx_on s6, gpr_idx(SRC0)",
+            "\ts_nop 0", "\tv_xor_b32 v45, v112, v45", "\ts_set_gpr_idx_idx s7", "\ts_nop 0",
+            "\tv_xor_b32 v44, v112, v44", "\ts_set_gpr_idx_off", ""]
+    assert M.check("\n".join(good)) == ([], 1)
+    no_nop = [ln for ln in good if ln != "\ts_nop 0"]
+    assert len(M.check("\n".join(no_nop))[0]) == 2
+    foreign = good[:4] + ["\tv_mov_b32 v3, v4"] + good[4:]
+    assert any("foreign" in p for _, p in M.check("\n".join(foreign))[0])
+    spill = good[:1] + ["\tv_writelane_b32 v100, s5, 3"] + good[1:]
+    assert any("spill" in p for _, p in M.check("\n".join(spill))[0])

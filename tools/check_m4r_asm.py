@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Build-time ISA check of the four-Russians folds (csrc/pir_m4r.h) in libpir_engine.so.
+
+Inside every GPR-index window (s_set_gpr_idx_on ... s_set_gpr_idx_off) only the fold's own
+instructions may appear: index changes, their wait state, and v_xor_b32 whose src0 (the indexed
+operand) is a combination register (v96-v127).  Every index change is followed directly by an
+s_nop (the stale-index hazard, tools/micro/scan_m4r.hip).  In the functions that fold, no SGPR
+spill lane (v_writelane_b32) lands in the combination registers.
+
+    python tools/check_m4r_asm.py [lib]
+"""
+import os
+import re
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from check_plane_asm import disassemble  # noqa: E402
+
+PINNED = range(96, 128)
+XOR_RE = re.compile(r"^\s*v_xor_b32(?:_e32)?\s+v(\d+),\s*v(\d+),\s*v(\d+)")
+WL_RE = re.compile(r"^\s*v_writelane_b32\s+v(\d+),")
+
+
+def op(ln):
+    return ln.strip().split("//", 1)[0].strip()
+
+
+def check(asm_text):
+    """[(function, problem)], number of index windows checked."""
+    lines = [ln for ln in asm_text.splitlines()]
+    bad, windows = [], 0
+    func, folds, inside = "?", False, False
+    spills = []
+    prev = ""
+    for ln in lines:
+        if ln.endswith(">:"):
+            if folds:
+                bad += [(func, s) for s in spills]
+            func, folds, inside, spills, prev = ln, False, False, [], ""
+            continue
+        o = op(ln)
+        if not o:
+            continue
+        m = WL_RE.match(o)
+        if m and int(m.group(1)) in PINNED:
+            spills.append(f"spill lane in a combination register: {o}")
+        if prev.startswith(("s_set_gpr_idx_on", "s_set_gpr_idx_idx")) and not o.startswith("s_nop"):
+            bad.append((func, f"no wait state after '{prev}': {o}"))
+        if o.startswith("s_set_gpr_idx_on"):
+            if inside:
+                bad.append((func, "nested index window"))
+            inside, folds = True, True
+            windows += 1
+        elif o.startswith("s_set_gpr_idx_off"):
+            inside = False
+        elif inside and not o.startswith(("s_set_gpr_idx_idx", "s_nop")):
+            x = XOR_RE.match(o)
+            if not x or int(x.group(2)) not in PINNED:
+                bad.append((func, f"foreign instruction in an index window: {o}"))
+        prev = o
+    if folds:
+        bad += [(func, s) for s in spills]
+    return bad, windows
+
+
+def main(argv):
+    lib = argv[1] if len(argv) > 1 else os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "erasurecodedpir_amd",
+        "libpir_engine.so")
+    bad, n = check(disassemble(lib))
+    print(f"{n} index windows checked, {len(bad)} problems")
+    for f, p in bad[:20]:
+        print(f, p)
+    return 1 if bad or not n else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv))
