@@ -431,6 +431,25 @@ __device__ __forceinline__ Chunk<VEC> load_chunk(const uint8_t* p) {
   return ch;
 }
 
+// the same through a buffer resource (nt): soff = the row's byte offset (wave-uniform), voff =
+// the lane's chunk offset; a load past num_records reads zeros without touching memory
+template <int VEC>
+__device__ __forceinline__ Chunk<VEC> load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32_t voff,
+                                                     uint32_t soff) {
+  Chunk<VEC> ch;
+  if constexpr (VEC == 4) {
+    const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 2);
+    ch.v[0] = q.x; ch.v[1] = q.y; ch.v[2] = q.z; ch.v[3] = q.w;
+  } else if constexpr (VEC == 2) {
+    const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 2);
+    ch.v[0] = q.x; ch.v[1] = q.y;
+  } else {
+    ch.v[0] = __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 2);
+  }
+  return ch;
+}
+constexpr int kBufRsrcWord3 = 0x00020000;  // gfx9 raw buffer: 32-bit data format, no swizzle
+
 // coefficient bytes of record i: nrp bytes at c + i*nrp, as 4 dwords
 template <int NRP>
 __device__ __forceinline__ uint4 load_coef(const uint8_t* c, uint64_t i) {
@@ -768,9 +787,10 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
           uint32_t vi = 0;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const uint32_t w = m4r_hi ? __builtin_amdgcn_readlane(c4.y, j0 + r)
-                                      : __builtin_amdgcn_readlane(c4.x, j0 + r);
-            vi |= ((w >> m4r_sh) & 1u) << r;
+            // both readlanes unconditionally (inside the ?: arms they became a divergent branch)
+            const uint32_t wx = __builtin_amdgcn_readlane(c4.x, j0 + r);
+            const uint32_t wy = __builtin_amdgcn_readlane(c4.y, j0 + r);
+            vi |= (((m4r_hi ? wy : wx) >> m4r_sh) & 1u) << r;
           }
           m4r_fold4<VEC, NQ>(Z, x[0].v, x[1].v, x[2].v, x[3].v, vi);
 #pragma unroll
@@ -1556,11 +1576,25 @@ __global__ __launch_bounds__(NT) void k_query(
     // Unconditional loads (straight-line code keeps each refill behind its fold): a slot with
     // no row reads the shard's first bytes instead, and its coefficient is 0 (or, past the last
     // tile, it is never folded; inactive lanes' planes are never written out).
+    // one record per wave row: buffer loads over the tile's rows (resource in SGPRs, num_records
+    // 0 past the queue's last tile), the row's byte offset in soffset (wave-uniform), the lane's
+    // chunk offset in voffset (lanes past the record read its first chunk) -- no per-lane 64-bit
+    // address arithmetic, exec masking or branch per row.  TILE * pitch < 2^31 (make_query_plan).
+    const uint8_t* const rgn = shard + (b * region_rows) * pitch;
+    const uint32_t lane_off = chunk < cpr ? chunk * CH : 0u;
+    const uint32_t tile_bytes = (uint32_t)TILE * pitch;
     auto load_slot = [&](uint32_t g, uint32_t j, Chunk<VEC>& dst) __attribute__((always_inline)) {
       const uint32_t gi = wi + j * nwg;
-      const uint32_t rl = gi * rpw + rec_off;
-      const bool ok = g < total && active && gi < ngroups && rl < TILE;
-      dst = load_chunk<VEC>(ok ? rbase + ((uint64_t)(g & (ntiles - 1)) * TILE + rl) * pitch : shard);
+      if constexpr (UNI) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(rgn + (uint64_t)(g & (ntiles - 1)) * tile_bytes), (short)0,
+            g < total ? (int)tile_bytes : 0, kBufRsrcWord3);
+        dst = load_chunk_buf<VEC>(rs, lane_off, gi < ngroups ? gi * pitch : 0u);
+      } else {
+        const uint32_t rl = gi * rpw + rec_off;
+        const bool ok = g < total && active && gi < ngroups && rl < TILE;
+        dst = load_chunk<VEC>(ok ? rbase + ((uint64_t)(g & (ntiles - 1)) * TILE + rl) * pitch : shard);
+      }
     };
     auto fold_row = [&](const Chunk<VEC>& xr, const uint4& c4) __attribute__((always_inline)) {
 #pragma unroll
@@ -1633,9 +1667,10 @@ __global__ __launch_bounds__(NT) void k_query(
               uint32_t vi = 0;
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const uint32_t w = m4r_hi ? __builtin_amdgcn_readlane(c4.y, g4 + r)
-                                          : __builtin_amdgcn_readlane(c4.x, g4 + r);
-                vi |= ((w >> m4r_sh) & 1u) << r;
+                // both readlanes unconditionally (inside the ?: arms they became a branch)
+                const uint32_t wx = __builtin_amdgcn_readlane(c4.x, g4 + r);
+                const uint32_t wy = __builtin_amdgcn_readlane(c4.y, g4 + r);
+                vi |= (((m4r_hi ? wy : wx) >> m4r_sh) & 1u) << r;
               }
               m4r_fold4<VEC, NQ>(Z, x[g4].v, x[g4 + 1].v, x[g4 + 2].v, x[g4 + 3].v, vi);
 #pragma unroll
@@ -2085,6 +2120,7 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
   }
   // 4-5 rounds at VEC 2 with one record per wave row: the four-Russians k_query (768 threads:
   // 4 tree + 8 scan waves) unless $PIR_QUERY_M4R=0
+  if ((uint64_t)tile * pitch >= (1ull << 31)) return qp;  // a tile's rows: one buffer resource
   qp.m4r = nq >= 4 && nq <= 5 && nq > PIR_QUERY_BRANCH_MAXNQ && tile == 1024 &&
            pitch / 8 >= (uint32_t)kColGroupLanes;
   if (const char* mv = getenv("PIR_QUERY_M4R")) qp.m4r = qp.m4r && atoi(mv) != 0;
