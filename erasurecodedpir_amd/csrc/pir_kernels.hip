@@ -450,6 +450,31 @@ __device__ __forceinline__ Chunk<VEC> load_chunk_buf(__amdgpu_buffer_rsrc_t r, u
 }
 constexpr int kBufRsrcWord3 = 0x00020000;  // gfx9 raw buffer: 32-bit data format, no swizzle
 
+// Four-Russians plane indices of a group of 4 rows (pir_m4r.h): lane k = plane (k / 8, k % 8)
+// takes bit k % 8 of the rows' round-k/8 coefficient bytes -- bit k of each row's 64-bit
+// coefficient word (rounds 0-7 little-endian), i.e. the word used as a lane mask: one
+// v_cndmask per row.  w_r = row r's word, wave-uniform.
+__device__ __forceinline__ uint32_t m4r_index(uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3) {
+  uint32_t vi, t;
+  asm("v_cndmask_b32_e64 %0, 0, 1, %2\n\t"
+      "v_cndmask_b32_e64 %1, 0, 2, %3\n\t"
+      "v_or_b32_e32 %0, %0, %1\n\t"
+      "v_cndmask_b32_e64 %1, 0, 4, %4\n\t"
+      "v_or_b32_e32 %0, %0, %1\n\t"
+      "v_cndmask_b32_e64 %1, 0, 8, %5\n\t"
+      "v_or_b32_e32 %0, %0, %1"
+      : "=&v"(vi), "=&v"(t)
+      : "s"(w0), "s"(w1), "s"(w2), "s"(w3));
+  return vi;
+}
+// row j's coefficient word from the lanes holding a 64-row block's coefficients (x: rounds 0-3,
+// y: rounds 4-7)
+__device__ __forceinline__ uint64_t coef_word(const uint4& c4, uint32_t j) {
+  // (readlane returns int: through uint32_t, or the low word would sign-extend into the high)
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane(c4.x, j) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(c4.y, j) << 32);
+}
+
 // coefficient bytes of record i: nrp bytes at c + i*nrp, as 4 dwords
 template <int NRP>
 __device__ __forceinline__ uint4 load_coef(const uint8_t* c, uint64_t i) {
@@ -774,9 +799,6 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
 #pragma unroll
     for (int u = 0; u < U; ++u) load_row(r0 + u, x[u]);
     uint4 c4 = coefs64(r0);
-    // kM4R: lane 8a + b builds plane (a, b)'s index from bit b of the round-a coefficient bytes
-    const uint32_t m4r_sh = 8u * ((lane >> 3) & 3u) + (lane & 7u);
-    const bool m4r_hi = lane >= 32;
     for (uint64_t rb = r0; rb < r1; rb += 64) {
       const uint4 c4n = coefs64(rb + 64);  // the next 64 rows' coefficients, in flight
       const uint32_t nb = (uint32_t)(r1 - rb < 64 ? r1 - rb : 64);
@@ -784,14 +806,8 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
         // groups of 4 rows; rows past the wave's last have zero coefficients (no plane takes
         // them) and re-read its first row
         for (uint32_t j0 = 0; j0 < nb; j0 += 4) {
-          uint32_t vi = 0;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            // both readlanes unconditionally (inside the ?: arms they became a divergent branch)
-            const uint32_t wx = __builtin_amdgcn_readlane(c4.x, j0 + r);
-            const uint32_t wy = __builtin_amdgcn_readlane(c4.y, j0 + r);
-            vi |= (((m4r_hi ? wy : wx) >> m4r_sh) & 1u) << r;
-          }
+          const uint32_t vi = m4r_index(coef_word(c4, j0), coef_word(c4, j0 + 1),
+                                        coef_word(c4, j0 + 2), coef_word(c4, j0 + 3));
           m4r_fold4<VEC, NQ>(Z, x[0].v, x[1].v, x[2].v, x[3].v, vi);
 #pragma unroll
           for (int r = 0; r < 4; ++r) load_row(rb + j0 + r + U, x[r]);
@@ -1559,9 +1575,6 @@ __global__ __launch_bounds__(NT) void k_query(
     // across tiles; several records per row: U rows loaded, then folded, per batch)
     constexpr int U = (kPlaneAsm || kM4R) ? PIR_PLANE_U : (SW >= 8 ? 8 : 16);
     static_assert(!kM4R || U % 4 == 0, "four Russians: groups of 4 rows");
-    // kM4R: lane 8a + b builds plane (a, b)'s index from bit b of the round-a coefficient bytes
-    const uint32_t m4r_sh = 8u * ((lane >> 3) & 3u) + (lane & 7u);
-    const bool m4r_hi = lane >= 32;
     // row slot j of a tile = row group wi + j * nwg; rpt slots per tile, a multiple of U (slots
     // past the tile's row groups are masked)
     const uint32_t rpt = ((ngroups + nwg - 1) / nwg + U - 1) / U * U;
@@ -1664,14 +1677,8 @@ __global__ __launch_bounds__(NT) void k_query(
           if constexpr (kM4R) {
 #pragma unroll
             for (int g4 = 0; g4 < U; g4 += 4) {
-              uint32_t vi = 0;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                // both readlanes unconditionally (inside the ?: arms they became a branch)
-                const uint32_t wx = __builtin_amdgcn_readlane(c4.x, g4 + r);
-                const uint32_t wy = __builtin_amdgcn_readlane(c4.y, g4 + r);
-                vi |= (((m4r_hi ? wy : wx) >> m4r_sh) & 1u) << r;
-              }
+              const uint32_t vi = m4r_index(coef_word(c4, g4), coef_word(c4, g4 + 1),
+                                            coef_word(c4, g4 + 2), coef_word(c4, g4 + 3));
               m4r_fold4<VEC, NQ>(Z, x[g4].v, x[g4 + 1].v, x[g4 + 2].v, x[g4 + 3].v, vi);
 #pragma unroll
               for (int r = 0; r < 4; ++r) load_slot(gn, jn + g4 + r, x[g4 + r]);
