@@ -54,6 +54,10 @@ class CClient(ctypes.Structure):  # include/pir_server.h `client` (src/c/client.
 
 
 # name -> (restype, argtypes)
+class U128(ctypes.Structure):  # uint128_t (utils.h:13-15) by value: two INTEGER eightbytes
+    _fields_ = [("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64)]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _U32 = ctypes.c_uint32
@@ -156,6 +160,30 @@ PROTOTYPES = {
                                                   ctypes.POINTER(c_u8_p)]),
     "calcShamirDPFKeyLength": (_I, [_I]),
     "calcShamirResponseLength": (_I, [_I, _I]),
+    # client-side names of package c (src/client, src/benchmark)
+    "generate_opt_DPF_tree_query": (None, [ctypes.POINTER(CClient), _I,
+                                           ctypes.POINTER(ctypes.POINTER(c_u8_p))]),
+    "generateHollantiQuery": (None, [ctypes.POINTER(CClient), _I,
+                                     ctypes.POINTER(ctypes.POINTER(c_u8_p))]),
+    "mac": (None, [_P, _P, _I, _P, _I]),
+    "choose": (_I, [_I, _I]),
+    "convertInt": (U128, [_I]),
+    "calcCDDPFKeyLength": (_I, [_I, _I, _I, _I, _I]),
+    "calcWoodruffKeyLength": (_I, [_I, _I, _I, _I, _I]),
+    "generateMultiPartyDPFQuery": (None, [ctypes.POINTER(CClient), _I,
+                                          ctypes.POINTER(ctypes.POINTER(c_u8_p))]),
+    "assembleMultiPartyResponses": (None, [ctypes.POINTER(CClient), _P,
+                                           ctypes.POINTER(ctypes.POINTER(c_u8_p)), _P]),
+    "generateCDQuery": (None, [ctypes.POINTER(CClient), _I,
+                               ctypes.POINTER(ctypes.POINTER(c_u8_p))]),
+    "assembleCDResponses": (None, [ctypes.POINTER(CClient), _P,
+                                   ctypes.POINTER(ctypes.POINTER(c_u8_p)), _P]),
+    "genShamirCoeffs": (None, [_I, _I, _I, U128, _P, _P]),
+    "genOptShamirDPF": (None, [_I, U128, _I, _I, _I, _P, _P, _P]),
+    "assembleShamirResponses": (None, [ctypes.POINTER(CClient), _P, _P, _P, _P, _P]),
+    "genWoodruffVs": (None, [_I, _I, _P]),
+    "genWoodruffQuery": (None, [U128, _I, _I, _I, _P, _P]),
+    "assembleWoodruffResponses": (None, [ctypes.POINTER(CClient), _P, _P, _P, _P]),
     "pirSetDevice": (None, [_I]),
     "pirServerShardChanged": (None, [ctypes.POINTER(CServer)]),
 }
@@ -163,7 +191,8 @@ PROTOTYPES = {
 GLOBALS_INT = ["NUM_PARTIES", "NUM_FILES", "NUM_ENCODED_FILES", "LOG_NUM_ENCODED_FILES",
                "ENCODED_PAYLOAD_SIZE_BYTES", "ENCODED_FILE_SIZE_BYTES", "ENCODE_ACROSS",
                "NUM_ROUNDS", "RHO", "K", "T", "R", "B", "NUM_RESPONSES", "MODE", "IS_HERMITE",
-               "D", "MAC_SIZE_BYTES", "CHECK_MAC", "NUM_RSS_KEYS", "NUM_CD_KEYS", "WOODRUFF_M",
+               "D", "MAC_SIZE_BYTES", "CHECK_MAC", "NUM_RSS_KEYS", "NUM_CD_KEYS",
+               "NUM_CD_KEYS_NEEDED", "WOODRUFF_M",
                "WOODRUFF_D", "WOODRUFF_DERIVATIVE"]
 GLOBALS_U32 = ["LOG_NUM_FILES", "FILE_SIZE_BYTES", "PAYLOAD_SIZE_BYTES"]
 

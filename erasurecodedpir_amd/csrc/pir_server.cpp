@@ -3,16 +3,19 @@
 // pir_engine_answer / pir_engine_answer_slice.
 #include "../../include/pir_server.h"
 
+#include <errno.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/random.h>
 
 #include <mutex>
 #include <random>
 #include <utility>
 #include <vector>
 
+#include "../../include/pir_client.h"
 #include "../../include/pir_engine.h"
 
 extern "C" {
@@ -40,6 +43,7 @@ int MAC_SIZE_BYTES = 32;
 int CHECK_MAC = 0;
 int NUM_RSS_KEYS = 0;  // params.cpp:39-46 defaults (CD / Woodruff modes are not served)
 int NUM_CD_KEYS = 0;
+int NUM_CD_KEYS_NEEDED = 0;
 int WOODRUFF_M = 0;
 int WOODRUFF_D = 0;
 int WOODRUFF_DERIVATIVE = 0;
@@ -192,6 +196,102 @@ std::vector<uint8_t> vandermonde_inverse(const uint8_t* pts, int m) {
     abort();
   }
   return inv;
+}
+
+// The OS CSPRNG (the reference draws key seeds and polynomial coefficients with RAND_bytes).
+void os_random(uint8_t* buf, size_t len) {
+  while (len) {
+    const ssize_t got = getrandom(buf, len, 0);
+    if (got < 0) {
+      if (errno == EINTR) continue;
+      perror("pir shim: getrandom");
+      abort();
+    }
+    buf += got;
+    len -= (size_t)got;
+  }
+}
+
+// SHA-256 (FIPS 180-4) and HMAC (RFC 2104), for mac() -- the reference calls OpenSSL's HMAC.
+struct Sha256 {
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                   0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint8_t blk[64];
+  size_t fill = 0;
+  uint64_t total = 0;
+  static uint32_t ror(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); }
+  void compress(const uint8_t* p) {
+    static const uint32_t k[64] = {
+        0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4,
+        0xab1c5ed5, 0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe,
+        0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f,
+        0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7,
+        0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc,
+        0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b,
+        0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116,
+        0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+        0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
+        0xc67178f2};
+    uint32_t w[64];
+    for (int i = 0; i < 16; ++i)
+      w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 |
+             (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+    for (int i = 16; i < 64; ++i) {
+      const uint32_t s0 = ror(w[i - 15], 7) ^ ror(w[i - 15], 18) ^ (w[i - 15] >> 3);
+      const uint32_t s1 = ror(w[i - 2], 17) ^ ror(w[i - 2], 19) ^ (w[i - 2] >> 10);
+      w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+    }
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+    for (int i = 0; i < 64; ++i) {
+      const uint32_t t1 = hh + (ror(e, 6) ^ ror(e, 11) ^ ror(e, 25)) + ((e & f) ^ (~e & g)) +
+                          k[i] + w[i];
+      const uint32_t t2 = (ror(a, 2) ^ ror(a, 13) ^ ror(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+  }
+  void update(const uint8_t* p, size_t n) {
+    total += n;
+    while (n) {
+      const size_t take = (64 - fill) < n ? (64 - fill) : n;
+      memcpy(blk + fill, p, take);
+      fill += take; p += take; n -= take;
+      if (fill == 64) { compress(blk); fill = 0; }
+    }
+  }
+  void final(uint8_t out[32]) {
+    const uint64_t bits = total * 8;
+    const uint8_t one = 0x80, zero = 0;
+    update(&one, 1);
+    while (fill != 56) update(&zero, 1);
+    uint8_t len[8];
+    for (int i = 0; i < 8; ++i) len[i] = (uint8_t)(bits >> (56 - 8 * i));
+    update(len, 8);
+    for (int i = 0; i < 8; ++i)
+      for (int j = 0; j < 4; ++j) out[4 * i + j] = (uint8_t)(h[i] >> (24 - 8 * j));
+  }
+};
+
+void hmac_sha256(const uint8_t* key, size_t klen, const uint8_t* msg, size_t mlen,
+                 uint8_t out[32]) {
+  uint8_t k0[64] = {0};
+  if (klen > 64) {
+    Sha256 s;
+    s.update(key, klen);
+    s.final(k0);
+  } else {
+    memcpy(k0, key, klen);
+  }
+  uint8_t ipad[64], opad[64], inner[32];
+  for (int i = 0; i < 64; ++i) { ipad[i] = k0[i] ^ 0x36; opad[i] = k0[i] ^ 0x5c; }
+  Sha256 si;
+  si.update(ipad, 64);
+  si.update(msg, mlen);
+  si.final(inner);
+  Sha256 so;
+  so.update(opad, 64);
+  so.update(inner, 32);
+  so.final(out);
 }
 
 }  // namespace
@@ -640,6 +740,124 @@ void encode_within_files_server(client* c, server* s) {
     }
   }
   if (s->ctx) static_cast<ShimState*>(s->ctx)->dirty = true;
+}
+
+// ---- client-side names of package c (src/client/*.go, src/benchmark/benchmark.go) ----------
+
+// client.cpp:144-153: finalCW = gf_pow(j, RHO*i) ^ 1, keys by genOptimizedDPF
+// (dpf_tree.cpp:142-274) -- on the GPU (pir_gen_keys, the engine's own AES), root seeds from the
+// OS CSPRNG (the reference: RAND_bytes).  (*keys)[j] receives party j's key.
+void generate_opt_DPF_tree_query(client* c, int index, uint8_t*** keys) {
+  (void)c;
+  if (T != 1) {  // client.cpp:145 assert(T == 1)
+    fprintf(stderr, "pir shim: generate_opt_DPF_tree_query needs T == 1 (got %d)\n", T);
+    abort();
+  }
+  const int p = NUM_PARTIES, nq = NUM_ROUNDS, n = LOG_NUM_ENCODED_FILES;
+  const int kl = calcOptimizedDPFTreeKeyLength(p, n, nq);
+  if (p < 2 || kl <= 0 || index < 0 || index >= NUM_ENCODED_FILES) {
+    fprintf(stderr, "pir shim: generate_opt_DPF_tree_query: index %d, p %d, n %d\n", index, p, n);
+    abort();
+  }
+  std::vector<uint8_t> fcw((size_t)nq * (p - 1)), seeds((size_t)p * 16),
+      out((size_t)p * kl);
+  pir_final_cw(p, nq, RHO, fcw.data());
+  os_random(seeds.data(), seeds.size());
+  if (pir_gen_keys(device_default(), n, (uint64_t)index, fcw.data(), p, nq, seeds.data(),
+                   out.data()) != PIR_OK)
+    die("generate_opt_DPF_tree_query");
+  for (int j = 0; j < p; ++j) memcpy((*keys)[j], out.data() + (size_t)j * kl, kl);
+}
+
+// client.cpp:201-203 -> genHollantiDPF (shamir_dpf.cpp:190-237): for round a and record x a
+// random polynomial of t random low coefficients whose coefficient t + (a+1)*RHO - 1 is
+// [x == index]; keys[q][a][x] = its value at q + 1 (evalPoly, shamir_dpf.cpp:10-17, Horner).
+// The reference's evalPoly is called with degree t + RHO*NUM_ROUNDS on an array of that many
+// bytes and so reads one byte past the allocation as the top coefficient; the intended
+// polynomial (that byte 0) is computed here.
+void generateHollantiQuery(client* c, int index, uint8_t*** keys) {
+  (void)c;
+  const int p = NUM_PARTIES, nq = NUM_ROUNDS, t = T, rho = RHO;
+  const long N = NUM_ENCODED_FILES;
+  std::vector<uint8_t> rnd((size_t)N * t);
+  for (int a = 0; a < nq; ++a) {
+    os_random(rnd.data(), rnd.size());
+    const int sec = t + (a + 1) * rho - 1;
+    for (int q = 0; q < p; ++q) {
+      const uint8_t xq = (uint8_t)(q + 1);
+      uint8_t xsec = 1;  // xq^sec
+      for (int e = 0; e < sec; ++e) xsec = gf_mul_h(xsec, xq);
+      uint8_t* dst = keys[q][a];
+      for (long x = 0; x < N; ++x) {
+        const uint8_t* r = &rnd[(size_t)x * t];
+        uint8_t v = 0;
+        for (int m = t - 1; m >= 0; --m) v = gf_mul_h(v, xq) ^ r[m];
+        dst[x] = v ^ (x == index ? xsec : 0);
+      }
+    }
+  }
+}
+
+// utils.cpp:32-34: HMAC-SHA256 under a 16-byte key.  Like the reference (HMAC() writes the
+// whole digest and stores its length through the outputLen argument), 32 bytes are written.
+void mac(uint8_t* key, uint8_t* input, int inputLen, unsigned char* output, int outputLen) {
+  (void)outputLen;
+  hmac_sha256(key, 16, input, (size_t)(inputLen > 0 ? inputLen : 0), output);
+}
+
+// utils.cpp:168-174
+int choose(int n, int k) { return k == 0 ? 1 : (n * choose(n - 1, k - 1)) / k; }
+
+// utils.cpp:221-223
+uint128_t convertInt(int x) { return (uint128_t)x; }
+
+// utils.cpp:118-129 (double pow as in the reference; ceil((double)(n/2)) == n/2)
+int calcCDDPFKeyLength(int p, int log_domainSize, int t, int num_cd_keys_needed,
+                       int num_cd_keys) {
+  (void)t;
+  const int n = log_domainSize;
+  const uint32_t p2 = (uint32_t)pow(2, num_cd_keys_needed - 1);
+  const int mu_pow = n / 2 + 3;
+  const uint64_t mu = (uint64_t)pow(2, mu_pow), nu = (uint64_t)pow(2, n - mu_pow);
+  return (int)(16 * p2 * nu + num_cd_keys * nu * p2 + p2 * mu);
+}
+
+// utils.cpp:145-153: the smallest m >= 3 with choose(m, 2) >= 2^logDomainSize
+int calcWoodruffKeyLength(int p, int r, int t, int logDomainSize, int fileSizeBytes) {
+  (void)p; (void)r; (void)t; (void)fileSizeBytes;
+  int m = 3;
+  while (choose(m, 2) < (1 << logDomainSize)) ++m;
+  return m;
+}
+
+// The other modes' client halves: their server modes are refused at setSystemParams, so a
+// client of this engine never reaches them (and the multiparty key generation of the reference
+// cannot make a usable key: DESIGN.md, reference defects).
+void generateMultiPartyDPFQuery(client*, int, uint8_t***) {
+  out_of_scope("generateMultiPartyDPFQuery", "multiparty key generation");
+}
+void assembleMultiPartyResponses(client*, uint8_t*, uint8_t***, uint8_t*) {
+  out_of_scope("assembleMultiPartyResponses", "multiparty decode");
+}
+void generateCDQuery(client*, int, uint8_t***) { out_of_scope("generateCDQuery", "covering-design"); }
+void assembleCDResponses(client*, uint8_t*, uint8_t***, uint8_t*) {
+  out_of_scope("assembleCDResponses", "covering-design");
+}
+void genShamirCoeffs(int, int, int, uint128_t, uint8_t***, uint8_t***) {
+  out_of_scope("genShamirCoeffs", "Shamir");
+}
+void genOptShamirDPF(int, uint128_t, int, int, int, uint8_t***, uint8_t***, uint8_t***) {
+  out_of_scope("genOptShamirDPF", "Shamir");
+}
+void assembleShamirResponses(client*, uint8_t*, uint8_t***, uint8_t*, uint8_t***, uint8_t***) {
+  out_of_scope("assembleShamirResponses", "Shamir");
+}
+void genWoodruffVs(int, int, uint8_t**) { out_of_scope("genWoodruffVs", "Woodruff"); }
+void genWoodruffQuery(uint128_t, int, int, int, uint8_t**, uint8_t**) {
+  out_of_scope("genWoodruffQuery", "Woodruff");
+}
+void assembleWoodruffResponses(client*, uint8_t*, uint8_t***, uint8_t*, uint8_t**) {
+  out_of_scope("assembleWoodruffResponses", "Woodruff");
 }
 
 }  // extern "C"

@@ -190,9 +190,57 @@ class Client:
         """Client decode (client.cpp:211-268); see the module function of the same name."""
         return assembleDPFTreeQueryResponses(erasure, responses, self.c)
 
+    def generate_opt_DPF_tree_query(self, index):
+        """client.cpp:144-153 (src/client/tree.go:55): NUM_PARTIES keys (GPU key generation)."""
+        return generate_opt_DPF_tree_query(index, self.c)
+
+    def generateHollantiQuery(self, index):
+        """client.cpp:201-203 (src/client/hollanti.go:37): (NUM_PARTIES, NUM_ROUNDS,
+        NUM_ENCODED_FILES) coefficient vectors."""
+        return generateHollantiQuery(index, self.c)
+
     def free_client(self):
         if self.c.unencoded_files:
             self._lib.free_client(ctypes.byref(self.c))
+
+
+def generate_opt_DPF_tree_query(index, c=None):
+    """The client's keys for record `index` under the current setSystemParams(mode 0): a list of
+    NUM_PARTIES calcOptimizedDPFTreeKeyLength-byte keys (client.cpp:144-153)."""
+    lib = _lib.load()
+    prm = params()
+    p = prm["NUM_PARTIES"]
+    kl = lib.calcOptimizedDPFTreeKeyLength(p, prm["LOG_NUM_ENCODED_FILES"], prm["NUM_ROUNDS"])
+    keys = np.zeros((p, kl), np.uint8)
+    kp = _row_ptrs(keys)
+    cl = c if c is not None else CClient()
+    lib.generate_opt_DPF_tree_query(ctypes.byref(cl), int(index),
+                                    ctypes.cast(ctypes.pointer(kp), ctypes.POINTER(ctypes.POINTER(c_u8_p))))
+    return [keys[j].tobytes() for j in range(p)]
+
+
+def generateHollantiQuery(index, c=None):
+    """Polynomial-PIR query for record `index` under the current setSystemParams(mode 3):
+    (NUM_PARTIES, NUM_ROUNDS, NUM_ENCODED_FILES) (client.cpp:201-203)."""
+    lib = _lib.load()
+    prm = params()
+    p, nq, N = prm["NUM_PARTIES"], prm["NUM_ROUNDS"], prm["NUM_ENCODED_FILES"]
+    keys = np.zeros((p, nq, N), np.uint8)
+    rows = [_row_ptrs(keys[q]) for q in range(p)]
+    outer = (ctypes.POINTER(c_u8_p) * p)(*[ctypes.cast(r, ctypes.POINTER(c_u8_p)) for r in rows])
+    cl = c if c is not None else CClient()
+    lib.generateHollantiQuery(ctypes.byref(cl), int(index), outer)
+    return keys
+
+
+def mac(key16, msg):
+    """utils.cpp:32-34: HMAC-SHA256 of msg under the 16-byte key (32 bytes)."""
+    k = np.frombuffer(bytes(key16), np.uint8).copy()
+    m = np.frombuffer(bytes(msg), np.uint8).copy() if len(msg) else np.zeros(1, np.uint8)
+    out = np.zeros(32, np.uint8)
+    _lib.load().mac(k.ctypes.data_as(ctypes.c_void_p), m.ctypes.data_as(ctypes.c_void_p),
+                    len(msg), out.ctypes.data_as(ctypes.c_void_p), 32)
+    return out.tobytes()
 
 
 def assembleDPFTreeQueryResponses(erasure, responses, c=None):

@@ -158,6 +158,49 @@ void assembleHollantiResponses(client *c, uint8_t *erasureIndexList, uint8_t ***
 void lagrangeInterpolationSemihonest(uint8_t *evalPoints, uint8_t numPoints, uint8_t *evals,
                                      uint8_t funcDegree, uint8_t *output);
 
+/* ---- client-side names of package c: the Go files of src/client and src/benchmark bind
+ *      the same SWIG package as the server (client.h:26-46, utils.h:22-48, shamir_dpf.h:4-6,
+ *      woodruff.h:9-11), so the drop-in declares them too. ---- */
+#ifndef SWIG
+typedef unsigned __int128 uint128_t; /* utils.h:13-15 */
+#endif
+extern int NUM_CD_KEYS_NEEDED;       /* params.h:55 (0: covering-design modes are not served) */
+/* client.cpp:144-153 (tree.go:55): finalCW gf_pow(j, RHO*i) ^ 1 and genOptimizedDPF
+ * (dpf_tree.cpp:142-274) on the GPU (pir_gen_keys), root seeds from the OS CSPRNG (the
+ * reference: RAND_bytes); (*keys)[j] = party j's calcOptimizedDPFTreeKeyLength-byte key. */
+void generate_opt_DPF_tree_query(client *c, int index, uint8_t ***keys);
+/* client.cpp:201-203 -> genHollantiDPF (shamir_dpf.cpp:190-237) (hollanti.go:37):
+ * keys[q][round][record] = value at q+1 of a random polynomial whose coefficient
+ * T + (round+1)*RHO - 1 is [record == index] (host side; see pir_server.cpp for the
+ * reference's one-byte over-read that is not inherited). */
+void generateHollantiQuery(client *c, int index, uint8_t ***keys);
+/* utils.cpp:32-34 (benchmark.go:198): HMAC-SHA256 under a 16-byte key; writes 32 bytes. */
+void mac(uint8_t *key, uint8_t *input, int inputLen, unsigned char *output, int outputLen);
+int choose(int n, int k);               /* utils.cpp:168-174 */
+uint128_t convertInt(int x);            /* utils.cpp:221-223 */
+int calcCDDPFKeyLength(int p, int log_domainSize, int t, int num_cd_keys_needed,
+                       int num_cd_keys); /* utils.cpp:118-129 */
+int calcWoodruffKeyLength(int p, int r, int t, int logDomainSize,
+                          int fileSizeBytes); /* utils.cpp:145-153 */
+/* The other modes' client halves (multiparty key generation and decode, CD, Shamir, Woodruff):
+ * their server modes are refused at setSystemParams; these abort with a message. */
+void generateMultiPartyDPFQuery(client *c, int index, uint8_t ***keys);
+void assembleMultiPartyResponses(client *c, uint8_t *erasureIndexList, uint8_t ***responses,
+                                 uint8_t *output);
+void generateCDQuery(client *c, int index, uint8_t ***keys);
+void assembleCDResponses(client *c, uint8_t *erasureIndexList, uint8_t ***responses,
+                         uint8_t *output);
+void genShamirCoeffs(int n, int t, int numRounds, uint128_t index, uint8_t ***coeffs_x,
+                     uint8_t ***coeffs_y);
+void genOptShamirDPF(int log_domainSize, uint128_t index, int t, int p, int numRounds,
+                     uint8_t ***key_output, uint8_t ***coeffs_x, uint8_t ***coeffs_y);
+void assembleShamirResponses(client *c, uint8_t *erasureIndexList, uint8_t ***responses,
+                             uint8_t *output, uint8_t ***coeffs_x, uint8_t ***coeffs_y);
+void genWoodruffVs(int t, int m, uint8_t **v);
+void genWoodruffQuery(uint128_t index, int t, int p, int m, uint8_t **v, uint8_t **key_output);
+void assembleWoodruffResponses(client *c, uint8_t *erasureIndexList, uint8_t ***responses,
+                               uint8_t *output, uint8_t **v);
+
 /* Engine device used by servers created after this call (default: $PIR_DEVICE or 0). */
 void pirSetDevice(int device);
 /* indexList rows were written by something other than encode_across_files_server: the next

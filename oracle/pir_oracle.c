@@ -306,6 +306,24 @@ void orc_xorshift_fill(uint64_t seed, uint8_t *buf, size_t len) {
     }
 }
 
+static uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+void orc_splitmix_fill(uint64_t seed, uint64_t row0, uint64_t rows, uint32_t efs, uint8_t *buf) {
+    for (uint64_t r = 0; r < rows; r++) {
+        const uint64_t gr = row0 + r;
+        uint8_t *row = buf + r * efs;
+        for (uint32_t b = 0; b < efs; b += 8) {
+            uint64_t z = splitmix64(seed ^ ((gr << 20) | (b >> 3)));
+            for (uint32_t k = 0; k < 8 && b + k < efs; k++) row[b + k] = (uint8_t)(z >> (8 * k));
+        }
+    }
+}
+
 /* ------------------------------------------------------------------------------------ */
 /* Client side: sizing, synthetic DB, encode-across, erasure decode                     */
 /* ------------------------------------------------------------------------------------ */

@@ -217,6 +217,32 @@ double ref_server_time_parallel(void* hv, const uint8_t* key, uint8_t* result, i
     return same ? dt : -dt;
 }
 
+// `count` independent runOptimizedDPFTreeQuery calls (server.cpp:96-134) at once, one thread
+// each: call i answers keys[i*kl ..] as party party1[i] into results[i*nq*efs ..].  Each thread
+// gets a shallow copy of the server with its own EVP context and partyIndex (the fields the
+// answer reads); the shard rows are shared read-only.  Used for the full-size goldens.
+void ref_server_answer_many(void* hv, const uint8_t* keys, int kl, const int* party1, int count,
+                            uint8_t* results) {
+    ref_srv* h = (ref_srv*)hv;
+    set_tree_globals(h->p, h->n, h->efs, h->nq);
+    std::vector<server> views(count, h->s);
+    for (int i = 0; i < count; i++) {
+        views[i].ctx = EVP_CIPHER_CTX_new();
+        views[i].partyIndex = party1[i];
+        views[i].isByzantine = 0;
+    }
+    std::vector<std::thread> th;
+    for (int i = 0; i < count; i++)
+        th.emplace_back([&, i] {
+            std::vector<uint8_t*> res(h->nq);
+            for (int a = 0; a < h->nq; a++)
+                res[a] = results + ((size_t)i * h->nq + a) * h->efs;
+            runOptimizedDPFTreeQuery(&views[i], (uint8_t*)keys + (size_t)i * kl, h->nq, res.data());
+        });
+    for (auto& t : th) t.join();
+    for (auto& v : views) EVP_CIPHER_CTX_free(v.ctx);
+}
+
 // params.cpp:467-642 sizing for tree mode: setSystemParams(L,f,t=1,k,r,b=0,rho,mac,mode=0)
 void ref_e2e_sizes(int L, int f, int k, int r, int rho, int* out5) {
     setSystemParams(L, f, 1, k, r, 0, rho, 0, 0);
@@ -358,6 +384,18 @@ void ref_hollanti_sizes(int L, int f, int t, int k, int r, int rho, int* out3) {
 }
 
 int ref_shamir_key_len(int n) { return calcShamirDPFKeyLength(n); }
+
+// client-side names of package c (src/client, src/benchmark): utils.cpp:32-34, 118-129, 145-174
+void ref_mac(uint8_t* key, uint8_t* input, int inputLen, uint8_t* out32) {
+    mac(key, input, inputLen, out32, 32);
+}
+int ref_cd_key_len(int p, int n, int t, int needed, int keys) {
+    return calcCDDPFKeyLength(p, n, t, needed, keys);
+}
+int ref_woodruff_key_len(int p, int r, int t, int n, int f) {
+    return calcWoodruffKeyLength(p, r, t, n, f);
+}
+int ref_choose(int n, int k) { return choose(n, k); }
 
 // ---- multiparty sqrt(N) DPF (mode 1) --------------------------------------------------------
 // utils.cpp:105-116

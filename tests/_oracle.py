@@ -110,6 +110,14 @@ def xorshift(seed, nbytes):
     return out
 
 
+def splitmix_shard(seed, row0, rows, efs):
+    """The engine's fill_shard_random bytes (k_fill_shard) for rows [row0, row0 + rows)."""
+    out = np.zeros(rows * efs, np.uint8)
+    lib().orc_splitmix_fill(ctypes.c_uint64(seed), ctypes.c_uint64(row0), ctypes.c_uint64(rows),
+                            ctypes.c_uint32(efs), P(out))
+    return out
+
+
 def tree_sizes(L, f, k, r, rho=1):
     s = (ctypes.c_int * 5)()
     lib().orc_tree_sizes(L, f, k, r, rho, s)

@@ -210,6 +210,65 @@ def fullsize():
     write("fullsize.json", {"shard_seed": SHARD_SEED, "cases": cases})
 
 
+FULL24_CASES = [  # name, p, n, efs, nq, shard seed, [(index, [parties])]
+    ("c24", 2, 24, 1024, 1, 0xC24, [((1 << 24) // 3, [0, 1]), ((1 << 24) - 1, [0])]),
+    ("c5", 8, 24, 1024, 5, 0xC5, [((1 << 24) // 3 + 5, [0, 1, 7]), (1234567, [0])]),
+    ("c3", 2, 24, 256, 1, 0xC3, [(0, [0, 1]), ((1 << 24) - 1, [0]), (9876543, [0, 1]),
+                                 ((1 << 23) + 3, [0])]),
+]
+
+
+def fullsize24():
+    """Reference answers at the full 2^24-row BASELINE shapes: north_star's 2^24 x 1 KiB (p=2),
+    configs[4]'s per-server shape (2^24 x 1 KiB, p=8, NUM_ROUNDS=5) and configs[2]'s
+    2^24 x 256 B.  The shard INPUT is the engine's device generator (fill_shard_random,
+    k_fill_shard: splitmix64 per 8 bytes), restated by the oracle (orc_splitmix_fill) so the GPU
+    tests fill the shard in HBM instead of uploading 16 GiB; the answers are the reference's own
+    runOptimizedDPFTreeQuery over that shard (ref_server_view, one thread per call)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    REF.ref_server_view.restype = ctypes.c_void_p
+    cases = []
+    for (name, p, n, efs, nq, seed, keyspec) in FULL24_CASES:
+        N = 1 << n
+        kl = REF.ref_key_len(p, n, nq)
+        fcw = final_cw(p, nq, 1, nq)
+        shard = O.splitmix_shard(seed, 0, N, efs)
+        h = REF.ref_server_view(p, 1, n, efs, nq, ptr(shard))
+        keys, calls = [], []
+        for (idx, parties) in keyspec:
+            kk = np.zeros(p * kl, np.uint8)
+            REF.ref_gen_opt_dpf(n, U64(idx), ptr(fcw), p, nq, ptr(kk))
+            keys.append(kk)
+            calls += [(len(keys) - 1, party) for party in parties]
+        kbuf = np.concatenate([keys[q][party * kl:(party + 1) * kl] for (q, party) in calls])
+        p1 = (ctypes.c_int * len(calls))(*[party + 1 for (_, party) in calls])
+        res = np.zeros(len(calls) * nq * efs, np.uint8)
+        t0 = __import__("time").time()
+        REF.ref_server_answer_many(ctypes.c_void_p(h), ptr(kbuf), kl, p1, len(calls), ptr(res))
+        dt = __import__("time").time() - t0
+        REF.ref_server_view_free(ctypes.c_void_p(h))
+        queries = []
+        for q, (idx, _) in enumerate(keyspec):
+            per = {}
+            for c, (qq, party) in enumerate(calls):
+                if qq == q:
+                    per[str(party)] = {"key": keys[q][party * kl:(party + 1) * kl].tobytes().hex(),
+                                       "answer": res[c * nq * efs:(c + 1) * nq * efs].tobytes().hex()}
+            queries.append({"index": idx, "parties": per})
+        # a few rows of the input, so the device generator is checked where it is used
+        rows = sorted({0, 1, N // 2 + 1, N - 1, keyspec[0][0]})
+        cases.append({"name": name, "p": p, "n": n, "efs": efs, "nq": nq, "shard_seed": seed,
+                      "final_cw": fcw.tobytes().hex(), "key_len": kl,
+                      "shard_sha256_first_mib": sha(shard[:1 << 20]),
+                      "sample_rows": {str(r): sha(shard[r * efs:(r + 1) * efs]) for r in rows},
+                      "queries": queries, "ref_seconds_parallel": round(dt, 1)})
+        del shard
+        print("fullsize24 case", name, "calls", len(calls), "%.1f s" % dt)
+    write("fullsize24.json", {"generator": "k_fill_shard splitmix64 (oracle orc_splitmix_fill)",
+                              "cases": cases})
+
+
 def hollanti():
     """Polynomial (Hollanti) PIR, mode 3: keys from generateHollantiQuery, encode-within shards,
     every party's runHollantiQuery answer and its T-thread assembled form, the decode."""
@@ -242,6 +301,28 @@ def hollanti():
         print("hollanti case", L, f, t, k, r, rho, "p", p, "nq", nq, "efs", efs)
     write("hollanti.json", {"cases": cases,
                             "shamir_key_len": {str(n): REF.ref_shamir_key_len(n) for n in (1, 2, 7, 10, 20, 25)}})
+
+
+def client_kats():
+    """The client/benchmark names of package c with deterministic outputs: mac (HMAC-SHA256,
+    utils.cpp:32-34), choose, calcCDDPFKeyLength, calcWoodruffKeyLength."""
+    rng = np.random.RandomState(7)
+    macs = []
+    for n in (0, 1, 31, 64, 100, 1000):
+        key = bytes(rng.randint(0, 256, 16, dtype=np.uint8))
+        msg = bytes(rng.randint(0, 256, n, dtype=np.uint8))
+        out = np.zeros(32, np.uint8)
+        REF.ref_mac(key, msg, n, ptr(out))
+        macs.append({"key": key.hex(), "msg": msg.hex(), "mac": out.tobytes().hex()})
+    choose = {f"{n},{k}": REF.ref_choose(n, k) for n in range(0, 17) for k in range(0, n + 1)}
+    cd = {f"{p},{n},{t},{a},{b}": REF.ref_cd_key_len(p, n, t, a, b)
+          for (p, n, t, a, b) in [(5, 10, 3, 4, 2), (7, 12, 3, 6, 3), (8, 16, 3, 5, 3),
+                                  (16, 11, 8, 6, 3)]}
+    wd = {f"{p},{r},{t},{n},{f}": REF.ref_woodruff_key_len(p, r, t, n, f)
+          for (p, r, t, n, f) in [(4, 1, 1, 4, 8), (6, 2, 2, 10, 64), (3, 0, 1, 16, 32),
+                                  (5, 1, 2, 20, 1024)]}
+    write("client_kat.json", {"mac": macs, "choose": choose, "cd_key_len": cd,
+                              "woodruff_key_len": wd})
 
 
 MP_CASES = [  # (p, t, n, efs, threads): shares per record 2/3/4/5/9, short rows, mu_pow > n
@@ -298,12 +379,14 @@ if __name__ == "__main__":
     REF.ref_blen.restype = ctypes.c_uint32
     for fn in (REF.ref_gf_mul, REF.ref_gf_pow, REF.ref_gf_inv):
         fn.restype = ctypes.c_uint8
-    what = sys.argv[1:] or ["prg", "gf", "dpf", "e2e", "thread", "fullsize", "hollanti", "mp"]
+    what = sys.argv[1:] or ["prg", "gf", "dpf", "e2e", "thread", "fullsize", "hollanti", "mp", "client"]
     if "prg" in what: prg_kats()
     if "gf" in what: gf_kats()
     if "dpf" in what: dpf_and_answers()
     if "e2e" in what: e2e()
     if "thread" in what: thread_defect()
     if "fullsize" in what: fullsize()
+    if "fullsize24" in what: fullsize24()
+    if "client" in what: client_kats()
     if "hollanti" in what: hollanti()
     if "mp" in what: mp()

@@ -53,6 +53,96 @@ def test_fullsize_golden(pir, ci):
             assert q[1].tobytes().hex() == ent["answer"], (p, n, efs, party)
 
 
+def _check_device_shard(e, case):
+    """The engine's device-filled shard equals the oracle's restatement of its generator
+    (orc_splitmix_fill), which is the input the reference answered in make_golden.py."""
+    efs = case["efs"]
+    first = e.get_shard(0, (1 << 20) // efs).reshape(-1)
+    assert O.sha(first) == case["shard_sha256_first_mib"]
+    for r, h in case["sample_rows"].items():
+        assert O.sha(e.shard_row(int(r))) == h, r
+    # rows the fixture does not list, against the oracle directly
+    rng = np.random.default_rng(case["shard_seed"])
+    for r in rng.integers(0, 1 << case["n"], 16):
+        assert np.array_equal(e.shard_row(int(r)), O.splitmix_shard(case["shard_seed"], int(r), 1, efs))
+
+
+def _golden24(name):
+    return next(c for c in O.golden("fullsize24.json")["cases"] if c["name"] == name)
+
+
+@pytest.mark.parametrize("name", ["c24", "c5"])
+def test_fullsize24_golden_query(pir, name):
+    """north_star's 2^24 x 1 KiB (p=2) and configs[4]'s per-server shape (2^24 x 1 KiB, p=8,
+    NUM_ROUNDS=5: the four-Russians k_query): the GPU answers -- single, queued, and the
+    XOR of 8 thread slices -- equal the reference's runOptimizedDPFTreeQuery (server.cpp:96-134)
+    on the same keys and shard bytes (tests/golden/fullsize24.json)."""
+    case = _golden24(name)
+    p, n, efs, nq = case["p"], case["n"], case["efs"], case["nq"]
+    with pir.Engine(p, 1, n, efs, nq) as e:
+        e.fill_shard_random(case["shard_seed"])
+        _check_device_shard(e, case)
+        by_party = {}
+        for q in case["queries"]:
+            for party_s, ent in q["parties"].items():
+                by_party.setdefault(int(party_s), []).append(ent)
+        for party, ents in sorted(by_party.items()):
+            e.set_party(party + 1)
+            keys = [bytes.fromhex(ent["key"]) for ent in ents]
+            want = [ent["answer"] for ent in ents]
+            for k, w in zip(keys, want):
+                assert e.answer(k).tobytes().hex() == w, (name, party)
+            got = e.answer_stream(keys + keys[:1])
+            for i, w in enumerate(want + want[:1]):
+                assert got[i].tobytes().hex() == w, (name, party, i)
+            acc = np.zeros((nq, efs), np.uint8)
+            for t in range(8):
+                acc ^= e.answer_slice(keys[0], t, 8)
+            assert acc.tobytes().hex() == want[0], (name, party, "slices")
+
+
+def test_fullsize24_golden_batch_c3(pir):
+    """configs[2] (2^24 x 256 B): the batched path (answer_batch, batch_group keys per shard
+    pass) over 128 keys, four of them the reference's golden party-0 keys placed in different
+    groups, plus the golden party-1 keys: those answers equal the reference's; every other key
+    satisfies the PIR property.  The queue (k_query) answers the golden keys too."""
+    case = _golden24("c3")
+    p, n, efs, nq = case["p"], case["n"], case["efs"], case["nq"]
+    fcw = np.frombuffer(bytes.fromhex(case["final_cw"]), np.uint8)
+    rng = np.random.default_rng(33)
+    nk = 128
+    slots = [0, 41, 86, 127]
+    gold = {0: [], 1: []}
+    for q in case["queries"]:
+        for party_s, ent in q["parties"].items():
+            gold[int(party_s)].append((q["index"], bytes.fromhex(ent["key"]), ent["answer"]))
+    assert len(gold[0]) == len(slots)
+    idxs = [int(i) for i in rng.choice(1 << n, nk, replace=False)]
+    pairs = [pir.gen_keys(n, i, p, nq, fcw=fcw) for i in idxs]
+    keys0 = [kk[0] for kk in pairs]
+    for s, (_, k, _) in zip(slots, gold[0]):
+        keys0[s] = k
+    tab = _gf_table(int(fcw[0]))
+    with pir.Engine(p, 1, n, efs, nq) as e:
+        e.fill_shard_random(case["shard_seed"])
+        _check_device_shard(e, case)
+        a0 = e.answer_batch(keys0)
+        for s, (_, _, w) in zip(slots, gold[0]):
+            assert a0[s].tobytes().hex() == w, s
+        q0 = e.answer_stream([k for (_, k, _) in gold[0]])
+        for i, (_, _, w) in enumerate(gold[0]):
+            assert q0[i].tobytes().hex() == w, i
+        e.set_party(2)
+        keys1 = [kk[1] for kk in pairs]
+        g1 = e.answer_batch([k for (_, k, _) in gold[1]] + keys1[:60])
+        for i, (_, _, w) in enumerate(gold[1]):
+            assert g1[i].tobytes().hex() == w, i
+        recs = [e.shard_row(i) for i in idxs[:60]]
+    bad = [j for j in range(60) if j not in slots and
+           not np.array_equal(a0[j][0] ^ g1[len(gold[1]) + j][0], tab[recs[j]])]
+    assert not bad, bad
+
+
 def test_c3_full_size_batch_128(pir):
     """configs[2]: 2^24 x 256 B, 128 batched keys (distinct indices): every key's party-1 ^
     party-2 answer is finalCW * record; the batched path equals the query queue."""

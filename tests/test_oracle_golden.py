@@ -112,3 +112,25 @@ def test_thread_variant_defect_and_intended_semantics():
     for t in range(T):
         acc ^= O.answer_slice(p, 1, n, efs, nq, key, shard, t, T)
     assert np.array_equal(acc, full)
+
+
+def test_fullsize24_fixture_inputs():
+    """tests/golden/fullsize24.json (reference answers at the full 2^24-row shapes): its shard
+    input is the oracle's restatement of the engine's device generator (orc_splitmix_fill) --
+    the first MiB and the sampled rows hash as recorded -- and every stored key has the
+    reference key length (utils.cpp:85-90) and this case's finalCW tail."""
+    for case in O.golden("fullsize24.json")["cases"]:
+        efs, seed = case["efs"], case["shard_seed"]
+        first = O.splitmix_shard(seed, 0, (1 << 20) // efs, efs)
+        assert O.sha(first) == case["shard_sha256_first_mib"], case["name"]
+        for r, h in case["sample_rows"].items():
+            assert O.sha(O.splitmix_shard(seed, int(r), 1, efs)) == h, (case["name"], r)
+        kl = O.key_len(case["p"], case["n"], case["nq"])
+        assert kl == case["key_len"]
+        fcw = bytes.fromhex(case["final_cw"])
+        assert fcw == O.final_cw(case["p"], case["nq"]).tobytes()
+        for q in case["queries"]:
+            for ent in q["parties"].values():
+                key = bytes.fromhex(ent["key"])
+                assert len(key) == kl
+                assert len(bytes.fromhex(ent["answer"])) == case["nq"] * efs

@@ -5,7 +5,10 @@ Inside every GPR-index window (s_set_gpr_idx_on ... s_set_gpr_idx_off) only the 
 instructions may appear: index changes, their wait state, and v_xor_b32 whose src0 (the indexed
 operand) is a combination register (v96-v127).  Every index change is followed directly by an
 s_nop (the stale-index hazard, tools/micro/scan_m4r.hip).  In the functions that fold, no SGPR
-spill lane (v_writelane_b32) lands in the combination registers.
+spill lane (v_writelane_b32) lands in the combination registers.  The windows leave M0 holding
+the index (s_set_gpr_idx_off does not restore it; the folds declare "m0" clobbered): after a
+window, no instruction may read M0 before something writes it again (linear order; loops are
+covered by the clobber, which makes the compiler re-materialise M0 where it needs it).
 
     python tools/check_m4r_asm.py [lib]
 """
@@ -19,6 +22,20 @@ from check_plane_asm import disassemble  # noqa: E402
 PINNED = range(96, 128)
 XOR_RE = re.compile(r"^\s*v_xor_b32(?:_e32)?\s+v(\d+),\s*v(\d+),\s*v(\d+)")
 WL_RE = re.compile(r"^\s*v_writelane_b32\s+v(\d+),")
+M0_TOKEN = re.compile(r"\bm0\b")
+# instructions that read M0 implicitly (LDS-DMA buffer loads, s_movrel, messages, GWS)
+M0_IMPLICIT = re.compile(r"^(s_movrel|s_sendmsg|ds_gws|s_ttracedata)|^(buffer|global)_load\S*.*\blds\b")
+
+
+def m0_access(o):
+    """'w' if the instruction writes M0, 'r' if it reads it, None otherwise."""
+    mnem, _, rest = o.partition(" ")
+    ops = [x.strip() for x in rest.split(",")] if rest else []
+    if mnem.startswith("s_set_gpr_idx_on") or (ops and ops[0] == "m0"):
+        return "w"
+    if any(M0_TOKEN.search(x) for x in ops[1:]) or M0_IMPLICIT.search(o):
+        return "r"
+    return None
 
 
 def op(ln):
@@ -32,11 +49,12 @@ def check(asm_text):
     func, folds, inside = "?", False, False
     spills = []
     prev = ""
+    m0_stale = False
     for ln in lines:
         if ln.endswith(">:"):
             if folds:
                 bad += [(func, s) for s in spills]
-            func, folds, inside, spills, prev = ln, False, False, [], ""
+            func, folds, inside, spills, prev, m0_stale = ln, False, False, [], "", False
             continue
         o = op(ln)
         if not o:
@@ -46,13 +64,19 @@ def check(asm_text):
             spills.append(f"spill lane in a combination register: {o}")
         if prev.startswith(("s_set_gpr_idx_on", "s_set_gpr_idx_idx")) and not o.startswith("s_nop"):
             bad.append((func, f"no wait state after '{prev}': {o}"))
+        if not inside and not o.startswith("s_set_gpr_idx_off"):
+            acc = m0_access(o)
+            if acc == "w":
+                m0_stale = False
+            elif acc == "r" and m0_stale:
+                bad.append((func, f"M0 read after an index window before it is rewritten: {o}"))
         if o.startswith("s_set_gpr_idx_on"):
             if inside:
                 bad.append((func, "nested index window"))
             inside, folds = True, True
             windows += 1
         elif o.startswith("s_set_gpr_idx_off"):
-            inside = False
+            inside, m0_stale = False, True
         elif inside and not o.startswith(("s_set_gpr_idx_idx", "s_nop")):
             x = XOR_RE.match(o)
             if not x or int(x.group(2)) not in PINNED:
