@@ -213,9 +213,9 @@ def generate_opt_DPF_tree_query(index, c=None):
     kl = lib.calcOptimizedDPFTreeKeyLength(p, prm["LOG_NUM_ENCODED_FILES"], prm["NUM_ROUNDS"])
     keys = np.zeros((p, kl), np.uint8)
     kp = _row_ptrs(keys)
+    arr = ctypes.cast(kp, ctypes.POINTER(c_u8_p))  # the Go caller's `keys` (**byte); it passes &keys
     cl = c if c is not None else CClient()
-    lib.generate_opt_DPF_tree_query(ctypes.byref(cl), int(index),
-                                    ctypes.cast(ctypes.pointer(kp), ctypes.POINTER(ctypes.POINTER(c_u8_p))))
+    lib.generate_opt_DPF_tree_query(ctypes.byref(cl), int(index), ctypes.pointer(arr))
     return [keys[j].tobytes() for j in range(p)]
 
 

@@ -11,7 +11,13 @@ of 16-B-per-lane streaming reads, MI355X_MICROARCH.md §HBM).
 
 Derived issue figures (per CU, over the kernel's GRBM_GUI_ACTIVE cycles): VALU instructions per
 SIMD per cycle against the SIMD's 0.5 (a wave64 VALU op occupies a SIMD-32 for 2 cycles), SALU
-and LDS instructions per CU per cycle; SQ_* cycle counters count quad-cycles on gfx950."""
+and LDS instructions per CU per cycle; SQ_* cycle counters count quad-cycles on gfx950.
+GRBM_GUI_ACTIVE is reported once per XCD and summed over the dispatch's 8 instances here, so the
+kernel's cycle count is that sum / 8 (round-2 summaries divided by nothing: their per-cycle rates
+were 8x low and their implied clock 8x high).
+
+    python tools/pmc_summary.py --reissue CFG ...   recompute the issue block of the committed
+                                                    profiles/pmc_<cfg>.json from its counters"""
 import csv
 import glob
 import json
@@ -20,6 +26,37 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CUS = 256
+XCDS = 8
+
+
+def issue_block(avg, avg_ns, algo):
+    gui = avg["GRBM_GUI_ACTIVE"] / XCDS  # per-XCD counter, summed over the 8 XCDs
+    d = {"gui_active_cycles": round(gui, 1), "gui_active_sum_over_xcds": avg["GRBM_GUI_ACTIVE"],
+         "shader_clock_GHz_implied": round(gui / avg_ns, 3)}
+    if "SQ_INSTS_VALU" in avg:
+        d["valu_insts_per_simd_per_cycle"] = round(avg["SQ_INSTS_VALU"] / (CUS * 4) / gui, 4)
+        d["valu_issue_share_of_peak_0.5"] = round(avg["SQ_INSTS_VALU"] / (CUS * 4) / gui / 0.5, 4)
+    for k in ("SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD"):
+        if k in avg:
+            d[k.lower().replace("sq_insts_", "") + "_insts_per_cu_per_cycle"] = round(avg[k] / CUS / gui, 4)
+    if "SQ_INSTS_VALU" in avg:
+        d["valu_insts_per_shard_dword"] = round(avg["SQ_INSTS_VALU"] * 64 / (algo / 4), 3)
+    if "SQ_INSTS_SALU" in avg:
+        d["salu_insts_per_shard_dword"] = round(avg["SQ_INSTS_SALU"] * 64 / (algo / 4), 3)
+    return d
+
+
+def reissue(cfgs):
+    for cfg in cfgs:
+        dst = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
+        out = json.load(open(dst))
+        avg = out.get("counters_per_launch", {})
+        if "GRBM_GUI_ACTIVE" not in avg:
+            continue
+        out["issue"] = issue_block(avg, out["kernel_avg_ns_rocprof"],
+                                   out["algorithmic_bytes_per_launch"])
+        json.dump(out, open(dst, "w"), indent=1)
+        print(cfg, out["issue"]["shader_clock_GHz_implied"], "GHz")
 
 
 def rows(pattern):
@@ -30,6 +67,8 @@ def rows(pattern):
 
 
 def main():
+    if sys.argv[1] == "--reissue":
+        return reissue(sys.argv[2:])
     cfg, qpl, nrec, efs = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     base = os.path.join(ROOT, "gpurun_out")
     stats = rows(os.path.join(base, f"prof_{cfg}", "**", "*kernel_stats.csv"))
@@ -63,20 +102,8 @@ def main():
                           "(MI355X_MICROARCH.md HBM): read bytes = 2 x FETCH_SIZE x 1024",
             "hbm_bytes_per_launch": int(hbm), "hbm_bytes_per_query": int(hbm / qpl),
             "traffic_over_algorithmic": round(hbm / algo, 4)})
-    gui = avg.get("GRBM_GUI_ACTIVE")
-    if gui:
-        d = {"gui_active_cycles": gui, "shader_clock_GHz_implied": round(gui / avg_ns, 3)}
-        if "SQ_INSTS_VALU" in avg:
-            d["valu_insts_per_simd_per_cycle"] = round(avg["SQ_INSTS_VALU"] / (CUS * 4) / gui, 4)
-            d["valu_issue_share_of_peak_0.5"] = round(avg["SQ_INSTS_VALU"] / (CUS * 4) / gui / 0.5, 4)
-        for k in ("SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD"):
-            if k in avg:
-                d[k.lower().replace("sq_insts_", "") + "_insts_per_cu_per_cycle"] = round(avg[k] / CUS / gui, 4)
-        if "SQ_INSTS_VALU" in avg:
-            d["valu_insts_per_shard_dword"] = round(avg["SQ_INSTS_VALU"] * 64 / (algo / 4), 3)
-        if "SQ_INSTS_SALU" in avg:
-            d["salu_insts_per_shard_dword"] = round(avg["SQ_INSTS_SALU"] * 64 / (algo / 4), 3)
-        out["issue"] = d
+    if "GRBM_GUI_ACTIVE" in avg:
+        out["issue"] = issue_block(avg, avg_ns, algo)
     dst = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
