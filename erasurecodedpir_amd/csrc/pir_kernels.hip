@@ -1758,13 +1758,18 @@ __global__ __launch_bounds__(NT) void k_query(
           // (vmcnt(0)) before the workgroup's ONE agent-scope counter add; the workgroup whose
           // add comes last XORs the slabs of every workgroup with sc1 loads (the hand-off of
           // MI355X_MICROARCH.md's first sc1 row: no L2 write-back or invalidate needed).
+          // The hand-off is also ordered by the memory model, not only by the cache flavour:
+          // release (agent) before the counter add, acquire (agent) in the last workgroup.
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           group_barrier(&sm.sbar, sgen, SW);
-          if (st == 0)
-            sm.lastq = __hip_atomic_fetch_add(qcnt + qy, 1u, __ATOMIC_RELAXED,
+          if (st == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            sm.lastq = __hip_atomic_fetch_add(qcnt + qy, 1u, __ATOMIC_ACQ_REL,
                                               __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+          }
           group_barrier(&sm.sbar, sgen, SW);
           if (lds_load(&sm.lastq)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             const uint32_t words = pitch / 4, P = (uint32_t)NQ * words, nth = SW * 64;
             const uint32_t S = P >= nth ? 1u : nth / P;  // threads per output word
             const uint32_t gx = gridDim.x;
@@ -2336,6 +2341,9 @@ ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus, in
   if (nq == 3 && sh.vec == 4 && pitch / 16 < (uint32_t)kColGroupLanes &&
       pitch / 8 >= (uint32_t)kColGroupLanes)
     sh.vec = 2;  // 3 rounds: a record per wave row at VEC = 2 (as before VEC = 4 took them)
+  else if (nq == 3 && sh.vec == 4 && pitch / 8 < (uint32_t)kColGroupLanes &&
+           pitch / 4 >= (uint32_t)kColGroupLanes)
+    sh.vec = 1;  // 3 rounds, 256-511 B: a record per wave row at VEC = 1
   sh.pitch = pitch;
   sh.cpr = pitch / (sh.vec * 4);
   sh.uniform = sh.cpr >= (uint32_t)kColGroupLanes;
@@ -2365,6 +2373,14 @@ static hipError_t scan_nq(const ScanShape& sh, const uint8_t* d_shard, uint64_t 
                           const uint8_t* d_c, uint8_t* d_slabs, int acc, hipStream_t s) {
   constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : (NQ <= 8 ? 8 : 16)));
   constexpr int VEC = NQ <= 3 ? 4 : (NQ <= 8 ? 2 : 1);
+  if constexpr (VEC == 4) {
+    if (sh.vec == 1) {  // 3 rounds, 256-511 B records: one per wave row at one dword per lane
+      if (!sh.uniform) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((k_scan_uni<NQ, NRP, 1>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
+                         nrec, sh.pitch, sh.cpr, d_c, d_slabs, acc);
+      return hipGetLastError();
+    }
+  }
   if constexpr (VEC > 1) {
     if (sh.vec == VEC / 2) {  // narrower records: one per wave row at half the width
       if (!sh.uniform) return hipErrorInvalidValue;

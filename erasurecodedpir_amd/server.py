@@ -88,7 +88,11 @@ class Server:
     def _hollanti(self, keys, thread):
         efs = _lib.global_int("ENCODED_FILE_SIZE_BYTES")
         nq = _lib.global_int("NUM_ROUNDS")
-        k = np.ascontiguousarray(np.asarray(keys, np.uint8).reshape(nq, -1))
+        N = _lib.global_int("NUM_ENCODED_FILES")
+        k = np.ascontiguousarray(np.asarray(keys, np.uint8))
+        if k.size != nq * N:  # the shim reads NUM_ROUNDS rows of NUM_ENCODED_FILES bytes
+            raise ValueError(f"Hollanti keys of {k.size} bytes, expected {nq} x {N}")
+        k = k.reshape(nq, N)
         out = np.zeros((nq, efs), np.uint8)
         kp = _row_ptrs(k)
         if thread is None:
@@ -109,6 +113,11 @@ class Server:
         efs = _lib.global_int("ENCODED_FILE_SIZE_BYTES")
         out = np.zeros((_lib.global_int("NUM_RSS_KEYS"), efs), np.uint8)
         k = np.frombuffer(bytes(key), np.uint8).copy()
+        need = calcMultiPartyOptDPFKeyLength(_lib.global_int("NUM_PARTIES"),
+                                             _lib.global_int("LOG_NUM_ENCODED_FILES"),
+                                             _lib.global_int("T"))
+        if k.size < need:  # the shim reads calcMultiPartyOptDPFKeyLength bytes
+            raise ValueError(f"multiparty key of {k.size} bytes, expected {need}")
         kp = k.ctypes.data_as(ctypes.c_void_p)
         if thread is None:
             self._lib.runOptimizedMultiPartyDPFQuery(ctypes.byref(self.s), kp, _row_ptrs(out))

@@ -117,7 +117,9 @@ def test_gpu_hollanti_golden_end_to_end(ci):
                                       (12, 256, 5), (11, 300, 8), (12, 400, 4), (10, 256, 6),
                                       (7, 256, 7),
                                       # two dwords per lane, 4-5 rounds: the 768-thread kernel
-                                      (12, 1024, 5), (11, 512, 4), (10, 2048, 5), (9, 1040, 5)])
+                                      (12, 1024, 5), (11, 512, 4), (10, 2048, 5), (9, 1040, 5),
+                                      # 3 rounds, 256-511 B: one record per row at VEC 1
+                                      (11, 256, 3), (10, 300, 3), (10, 508, 3)])
 def test_gpu_answer_coefs_vs_oracle(n, efs, nq):
     import erasurecodedpir_amd as pir
     rng = np.random.default_rng(n * 131 + nq)
