@@ -505,8 +505,7 @@ def main():
     eng = pir.Engine(p, 1, n, efs, nq, device=local, log_num_partitions=g, partition_index=rank)
     eng.fill_shard_random(SHARD_SEED)
     if world > 1 and not rehearsal:
-        uid = broadcast_bytes(pir.comm_unique_id() if rank == 0 else None)
-        eng.attach_comm(uid, world, rank)
+        attach_or_exit(pir, eng, world, rank)
     m = measure(ctx, eng, [ks[0] for _, ks in keyset], W, K, single=not args.queue_only)
     if rehearsal and not args.queue_only:
         m["answers"], m["singles"] = ctx.fold(m["answers"]), ctx.fold(m["singles"])
@@ -637,6 +636,40 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def attach_or_exit(pir, eng, world, rank):
+    """Attach the RCCL communicator on every rank, or fail fast: the engine's init is
+    non-blocking and bounded ($PIR_COMM_INIT_TIMEOUT, pir_comm_attach), every rank reports its
+    outcome over gloo, and if any rank failed ALL ranks exit with status 3 and a message
+    (no retry, no re-exec)."""
+    import torch.distributed as dist
+    from erasurecodedpir_amd.dist import broadcast_bytes
+
+    err, uid = None, None
+    if rank == 0:
+        try:
+            uid = pir.comm_unique_id()
+        except Exception as ex:  # noqa: BLE001 -- reported below, on every rank
+            err = f"ncclGetUniqueId: {ex}"
+    uid = broadcast_bytes(uid)
+    if uid is None and err is None:
+        err = "no unique id from rank 0"
+    if err is None:
+        try:
+            eng.attach_comm(uid, world, rank)
+        except Exception as ex:  # noqa: BLE001
+            err = f"{type(ex).__name__}: {ex}"
+    errs = [None] * world
+    dist.all_gather_object(errs, err)
+    bad = [(r, e) for r, e in enumerate(errs) if e]
+    if bad:
+        if rank == 0:
+            print(f"bench.py: RCCL communicator init failed on {len(bad)} of {world} ranks: "
+                  + "; ".join(f"rank {r}: {e}" for r, e in bad), file=sys.stderr, flush=True)
+        eng.close()
+        dist.destroy_process_group()
+        sys.exit(3)
 
 
 def extra_leg(ctx, pir, config, W, K, rng, single=True):
@@ -788,9 +821,8 @@ def run_batch(args, ctx, config):
     n = n_local + g
     eng = pir.Engine(p, 1, n, efs, nq, device=local, log_num_partitions=g, partition_index=rank)
     eng.fill_shard_random(SHARD_SEED)
-    if world > 1:
-        uid = broadcast_bytes(pir.comm_unique_id() if rank == 0 else None)
-        eng.attach_comm(uid, world, rank)
+    if world > 1 and not getattr(ctx, "rehearsal", False):
+        attach_or_exit(pir, eng, world, rank)
     rng = np.random.default_rng(int.from_bytes(
         broadcast_bytes(os.urandom(8) if rank == 0 else None) if world > 1 else os.urandom(8), "little"))
     keyset, fcw = make_keys(pir, n, p, nq, nk, rng, local)

@@ -14,7 +14,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -49,6 +51,28 @@ int fail(int code, const char* fmt, ...) {
   do {                                                                                        \
     ncclResult_t _r = (expr);                                                                 \
     if (_r != ncclSuccess) return fail(PIR_ECOMM, "%s failed: %s", #expr, ncclGetErrorString(_r)); \
+  } while (0)
+
+// The engine's communicators are non-blocking (ncclConfig_t.blocking = 0), so that a refused or
+// stuck rank cannot hang the others inside ncclCommInitRank: a call may return ncclInProgress,
+// settled here by polling ncclCommGetAsyncError, bounded by timeout_s.
+ncclResult_t rccl_settle(ncclComm_t comm, ncclResult_t r, double timeout_s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (r == ncclInProgress) {
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+      return ncclInProgress;
+    std::this_thread::yield();
+    if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) return ncclSystemError;
+  }
+  return r;
+}
+
+#define RCCL_CALL(comm, expr)                                                                 \
+  do {                                                                                        \
+    ncclResult_t _r = rccl_settle((comm), (expr), 60.0);                                       \
+    if (_r != ncclSuccess)                                                                    \
+      return fail(PIR_ECOMM, "%s failed: %s", #expr,                                          \
+                  _r == ncclInProgress ? "timed out after 60 s" : ncclGetErrorString(_r));    \
   } while (0)
 
 int ilog2_exact(uint64_t v) {
@@ -514,7 +538,7 @@ int answer_dev_locked(pir_engine* e, const uint8_t* d_key, uint8_t* d_result, hi
                        part_out, s);
   if (rc) return rc;
   if (e->comm) {
-    RCCL_TRY(ncclAllGather(e->d_part, e->d_gather, out_bytes, ncclUint8, e->comm, s));
+    RCCL_CALL(e->comm, ncclAllGather(e->d_part, e->d_gather, out_bytes, ncclUint8, e->comm, s));
     HIP_TRY(pir::launch_xor_fold(e->d_gather, e->nranks, out_bytes, d_result, s));
   }
   if (ev) HIP_TRY(hipEventRecord(ev[EV_END], s));
@@ -551,7 +575,7 @@ int answer_batch_locked(pir_engine* e, const uint8_t* d_keys, int nk, uint8_t* d
                              part_out, s);
   if (rc) return rc;
   if (e->comm) {
-    RCCL_TRY(ncclAllGather(e->d_bpart, e->d_bgather, total, ncclUint8, e->comm, s));
+    RCCL_CALL(e->comm, ncclAllGather(e->d_bpart, e->d_bgather, total, ncclUint8, e->comm, s));
     HIP_TRY(pir::launch_xor_fold(e->d_bgather, e->nranks, total, d_result, s));
   }
   return PIR_OK;
@@ -594,7 +618,7 @@ int answer_stream_locked(pir_engine* e, const uint8_t* d_keys, int nk, uint8_t* 
                         part_out, s);
   if (rc) return rc;
   if (e->comm) {
-    RCCL_TRY(ncclAllGather(e->d_bpart, e->d_bgather, total, ncclUint8, e->comm, s));
+    RCCL_CALL(e->comm, ncclAllGather(e->d_bpart, e->d_bgather, total, ncclUint8, e->comm, s));
     HIP_TRY(pir::launch_xor_fold(e->d_bgather, e->nranks, total, d_result, s));
   }
   if (e->ev) HIP_TRY(hipEventRecord(e->ev[EV_END], s));
@@ -623,7 +647,7 @@ int answer_coefs_locked(pir_engine* e, const uint8_t* src, uint64_t pitch, uint6
     HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, out, s));
   }
   if (e->comm) {
-    RCCL_TRY(ncclAllGather(e->d_part, e->d_gather, out_bytes, ncclUint8, e->comm, s));
+    RCCL_CALL(e->comm, ncclAllGather(e->d_part, e->d_gather, out_bytes, ncclUint8, e->comm, s));
     HIP_TRY(pir::launch_xor_fold(e->d_gather, e->nranks, out_bytes, d_result, s));
   }
   return PIR_OK;
@@ -656,7 +680,7 @@ int answer_mp_locked(pir_engine* e, const pir::MpLayout& L, const uint8_t* d_key
     HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, out, s));
   }
   if (e->comm) {
-    RCCL_TRY(ncclAllGather(e->d_part, e->d_gather, out_bytes, ncclUint8, e->comm, s));
+    RCCL_CALL(e->comm, ncclAllGather(e->d_part, e->d_gather, out_bytes, ncclUint8, e->comm, s));
     HIP_TRY(pir::launch_xor_fold(e->d_gather, e->nranks, out_bytes, d_result, s));
   }
   return PIR_OK;
@@ -1349,7 +1373,22 @@ int pir_comm_attach(pir_engine_t* e, const uint8_t id[PIR_COMM_ID_BYTES], int nr
   HIP_TRY(hipSetDevice(e->cfg.device));
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
-  RCCL_TRY(ncclCommInitRank(&e->comm, nranks, u, rank));
+  // non-blocking init, bounded: a rank that cannot join (e.g. RCCL refuses the device) fails
+  // here with PIR_ECOMM after at most $PIR_COMM_INIT_TIMEOUT seconds (default 120) instead of
+  // leaving the other ranks blocked in ncclCommInitRank
+  const char* ts = getenv("PIR_COMM_INIT_TIMEOUT");
+  const double timeout_s = ts ? atof(ts) : 120.0;
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclComm_t comm = nullptr;
+  ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, u, rank, &cfg);
+  if (comm) r = rccl_settle(comm, r, timeout_s);
+  if (r != ncclSuccess) {
+    if (comm) (void)ncclCommAbort(comm);
+    return fail(PIR_ECOMM, "ncclCommInitRank(rank %d of %d) failed: %s", rank, nranks,
+                r == ncclInProgress ? "timed out" : ncclGetErrorString(r));
+  }
+  e->comm = comm;
   e->nranks = nranks;
   e->rank = rank;
   HIP_TRY(hipMalloc(&e->d_gather, (size_t)nranks * e->cfg.num_rounds * e->cfg.record_bytes));
