@@ -821,6 +821,8 @@ def run_batch(args, ctx, config):
     n = n_local + g
     eng = pir.Engine(p, 1, n, efs, nq, device=local, log_num_partitions=g, partition_index=rank)
     eng.fill_shard_random(SHARD_SEED)
+    if os.environ.get("PIR_BENCH_BATCH_G"):  # diagnostics: keys per shard pass
+        eng.batch_group = int(os.environ["PIR_BENCH_BATCH_G"])
     if world > 1 and not getattr(ctx, "rehearsal", False):
         attach_or_exit(pir, eng, world, rank)
     rng = np.random.default_rng(int.from_bytes(

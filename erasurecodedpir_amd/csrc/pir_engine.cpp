@@ -249,7 +249,7 @@ int answer_fused(pir_engine* e, const uint8_t* d_raw, int log_parts_total, uint6
   const pir::DevKey* d_key = e->d_keys;
   const auto& c = e->cfg;
   const pir::TreePlan pl =
-      pir::make_plan(c.log_num_records, log_parts_total, prefix, pir::fused_k(tile));
+      pir::make_plan(c.log_num_records, log_parts_total, prefix, pir::fused_k(tile), c.num_parties);
   const pir::ScanShape sh =
       pir::make_fused_shape(pl.nleaves, e->pitch, c.num_rounds, e->num_cus, tile);
   int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
@@ -339,7 +339,7 @@ int answer_core(pir_engine* e, const uint8_t* d_raw, int log_parts_total, uint64
   const int tile = e->allow_fused ? pir::fused_tile(c.num_rounds, e->pitch, nleaves, e->num_cus) : 0;
   if (tile) return answer_fused(e, d_raw, log_parts_total, prefix, row0, d_out, s, tile);
   e->last_fused = 0;
-  const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix);
+  const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix, -1, c.num_parties);
   const int C = pick_chunks(pl, e->num_cus);
   e->last_chunks = C;
   const uint64_t nrec = pl.nleaves / C;
@@ -397,7 +397,7 @@ int answer_batch_core(pir_engine* e, const uint8_t* d_raw, int nk, int log_parts
   e->last_batch_group = G;
   e->last_fused = 0;
   e->last_chunks = 1;
-  const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix, e->batch_k_last);
+  const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix, e->batch_k_last, c.num_parties);
   const pir::ScanShape sh =
       pir::make_scan_shape(pl.nleaves, e->pitch, W, e->num_cus, e->batch_scan_bpc);
   const size_t cb_bytes = (size_t)pl.nleaves * W;
@@ -761,12 +761,13 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
       return cleanup(fail(PIR_EHIP, "hipEventCreate failed"));
   pir::upload_aes_table(e->stream);
   pir::upload_mp_aes_table(e->stream);
+  pir::upload_leaves_aes_table(e->stream);
   const size_t shard_bytes = (size_t)e->rows * e->pitch;
   if (hipMalloc(&e->d_shard, shard_bytes) != hipSuccess)
     return cleanup(fail(PIR_ENOMEM, "hipMalloc shard %zu bytes", shard_bytes));
   if (hipMemsetAsync(e->d_shard, 0, shard_bytes, e->stream) != hipSuccess)
     return cleanup(fail(PIR_EHIP, "hipMemset shard"));
-  pir::TreePlan pl = pir::make_plan(c.log_num_records, c.log_num_partitions, 0);
+  pir::TreePlan pl = pir::make_plan(c.log_num_records, c.log_num_partitions, 0, -1, c.num_parties);
   {
     const char* f = getenv("PIR_FUSED");
     e->allow_fused = !(f && f[0] == '0');
@@ -783,7 +784,7 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
     const int tile = pir::fused_tile(c.num_rounds, e->pitch, e->rows, e->num_cus);
     if (tile) {
       const pir::TreePlan pf =
-          pir::make_plan(c.log_num_records, c.log_num_partitions, 0, pir::fused_k(tile));
+          pir::make_plan(c.log_num_records, c.log_num_partitions, 0, pir::fused_k(tile), c.num_parties);
       if (pf.max_nodes > pl.max_nodes) pl = pf;
     }
   }
@@ -1164,7 +1165,7 @@ int pir_engine_eval_all(pir_engine_t* e, const uint8_t* key, uint8_t* out) {
   memcpy(e->h_key, key, e->key_len);
   HIP_TRY(hipMemcpyAsync(e->d_key_raw, e->h_key, e->key_len, hipMemcpyHostToDevice, e->stream));
   const pir::TreePlan pl =
-      pir::make_plan(c.log_num_records, c.log_num_partitions, (uint64_t)c.partition_index);
+      pir::make_plan(c.log_num_records, c.log_num_partitions, (uint64_t)c.partition_index, -1, c.num_parties);
   HIP_TRY(pir::launch_frontier(pl, key_src(e, e->d_key_raw), e->nodes, e->stream));
   HIP_TRY(pir::launch_stages(pl, e->d_keys, e->nodes, 0, 1, e->d_c, e->nrp, e->stream));
   std::vector<uint8_t> ct((size_t)e->rows * e->nrp);
@@ -1266,7 +1267,7 @@ int pir_engine_profile_phases(pir_engine_t* e, const uint8_t* d_key, int iters, 
   if (int rc = ws_acquire(e, s)) return rc;
   e->ws_stream = nullptr;  // synchronised below
   const pir::TreePlan pl =
-      pir::make_plan(c.log_num_records, c.log_num_partitions, (uint64_t)c.partition_index);
+      pir::make_plan(c.log_num_records, c.log_num_partitions, (uint64_t)c.partition_index, -1, c.num_parties);
   const pir::ScanShape sh = pir::make_scan_shape(pl.nleaves, e->pitch, c.num_rounds, e->num_cus);
   int rc = ensure_slabs(e, (size_t)sh.grid.x * sh.grid.y * sh.slab_bytes);
   if (rc) return rc;

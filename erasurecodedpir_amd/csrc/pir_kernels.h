@@ -36,6 +36,7 @@ struct Stage {
 };
 struct TreePlan {
   int n, log_parts;
+  int p;  // parties (the control-bit bytes a node reads); 0: unknown (all 4 bytes)
   uint64_t prefix;
   int F, g, e;  // frontier: 2^g workgroups, each descends log_parts+g levels, expands e
   uint64_t nfront, nleaves, max_nodes;
@@ -48,7 +49,7 @@ struct NodeBufs {  // ping-pong node arrays in global memory (max_nodes entries 
 };
 
 // k_last: levels of the leaf-converting last stage (-1: default 4 for k_expand<FINAL>)
-TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last = -1);
+TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last = -1, int p = 0);
 int final_stage_blocks(const TreePlan& pl);  // workgroups of the leaf-converting stage
 
 void upload_aes_table(hipStream_t s);  // Te0 (computed on the host) -> __constant__ memory
@@ -83,6 +84,20 @@ hipError_t launch_frontier(const TreePlan& pl, const KeySrc& ks, const NodeBufs&
 hipError_t launch_stages(const TreePlan& pl, const DevKey* d_key, const NodeBufs& nb, int j, int C,
                          uint8_t* d_c, int nrp, hipStream_t s, int i0 = 0, int i1 = -1,
                          int cstride = 0, const StageBatch* batch = nullptr);
+// k_leaves (pir_leaves.hip): the leaf-converting last stage of kd levels, depth first per lane
+// (one input node per lane, its 2^kd leaves in registers; 4-table AES, pir_aes4.h); kd in
+// [kLeavesMinK, kLeavesMaxK], p = parties (the control-bit bytes a node needs).
+// Same arguments as a final k_expand stage: nkeys keys along grid y, input nodes in_stride
+// apart per key, key y's shares at c + y * c_key_off, leaf i's nrp bytes at c + i * cstride.
+constexpr int kLeavesMinK = 4;
+constexpr int kLeavesMaxK = 5;
+bool leaves_supported(int kd);
+hipError_t launch_leaves(int p, int nrp, int kd, const DevKey* d_key, const uint4* is,
+                         const uint32_t* it, int L0, uint64_t nin, int nkeys, uint64_t in_stride,
+                         uint8_t* c, uint32_t cstride, uint32_t c_key_off, hipStream_t s);
+void upload_leaves_aes_table(hipStream_t s);
+// $PIR_LEAF_DFS=0: final stages on k_expand<FINAL> (breadth first) instead of k_leaves
+bool leaf_dfs_enabled();
 // scan rows [0, nrec) of `shard` (row pitch `pitch`) with coefficients cT[i*nrp + a]
 struct ScanShape {
   int nq, nrp, vec;      // vec = dwords per lane chunk (4, 2, 1)

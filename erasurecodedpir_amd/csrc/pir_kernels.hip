@@ -16,6 +16,7 @@
 // HBM stream costs ~1 VALU op per byte.
 #include "pir_kernels.h"
 #include "pir_aes.h"
+#include "pir_tree.h"
 #include "pir_m4r.h"
 
 #include <algorithm>
@@ -75,30 +76,6 @@ __global__ __launch_bounds__(256) void k_key_prep(const uint8_t* __restrict__ ra
   parse_key(raw + blockIdx.x * key_stride, p, n, nq, party0, out + blockIdx.x);
 }
 
-// ------------------------------------------------------------------------------------------
-// Correction words of one level for a node with control bits t (dpf_tree.cpp:533-541):
-//   cs = XOR_{j: t_j} sCW[L][j]   (applied to both child seeds)
-//   ct = XOR_{j: t_j} tCW[L][j]   (applied to the packed child control bits)
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void level_cw(const DevKey* __restrict__ K, int L, uint32_t t,
-                                         uint32_t pm1, uint4& cs, uint32_t& ct) {
-  cs = make_uint4(0, 0, 0, 0);
-  ct = 0;
-  for (uint32_t j = 0; j < pm1; ++j) {
-    const uint32_t m = 0u - ((t >> j) & 1u);
-    cs = xor4(cs, and4(K->scw[L * kMaxCW + j], m));
-    ct ^= K->tcw[L * kMaxCW + j] & m;
-  }
-}
-
-struct Bits {
-  uint32_t pm1, tmask, tb_mask;
-  __device__ explicit Bits(uint32_t p) {
-    pm1 = p - 1;
-    tmask = (1u << pm1) - 1u;
-    tb_mask = 2 * pm1 >= 32 ? 0xffffffffu : ((1u << (2 * pm1)) - 1u);
-  }
-};
 
 // ------------------------------------------------------------------------------------------
 // k_frontier: the narrow, latency-bound top of the tree.  Each of 2^g workgroups descends from
@@ -270,44 +247,6 @@ struct ExpSmem {
   uint32_t tb[kExpOut / 4];
 };
 
-// G(seed) of an internal node with corrections: children seeds and control bits
-__device__ __forceinline__ void expand_node(const Tab& T, const DevKey* __restrict__ K, int L,
-                                            const Bits& B, uint4 seed, uint32_t t, uint4& sl,
-                                            uint4& sr, uint32_t& tl, uint32_t& tr) {
-  uint4 o[3];
-  aes_ctr_row<3, 1>(T, seed, o);
-  uint4 cs;
-  uint32_t ct;
-  level_cw(K, L, t, B.pm1, cs, ct);
-  sl = xor4(o[0], cs);
-  sr = xor4(o[1], cs);
-  const uint32_t tb = (o[2].x & B.tb_mask) ^ ct;
-  tl = tb & B.tmask;
-  tr = (tb >> B.pm1) & B.tmask;
-}
-
-// NRP bytes of leaf `leaf` at c + leaf * cstride (cstride = NRP, or a multiple of it when the
-// shares of several keys are interleaved per leaf for a batched scan)
-template <int NRP>
-__device__ __forceinline__ void store_leaf(uint8_t* __restrict__ c, uint64_t leaf, uint4 v,
-                                           uint32_t cstride = NRP) {
-  uint8_t* dst = c + leaf * cstride;
-  if constexpr (NRP == 1) *dst = (uint8_t)v.x;
-  else if constexpr (NRP == 2) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)v.x;
-  else if constexpr (NRP == 4) *reinterpret_cast<uint32_t*>(dst) = v.x;
-  else if constexpr (NRP == 8) *reinterpret_cast<uint2*>(dst) = make_uint2(v.x, v.y);
-  else *reinterpret_cast<uint4*>(dst) = v;
-}
-
-// leaf value (before masking to nq bytes)
-template <int NW>
-__device__ __forceinline__ uint4 leaf_value(const Tab& T, const DevKey* __restrict__ K,
-                                            uint32_t pm1, uint4 seed, uint32_t t) {
-  uint4 o[1];
-  aes_ctr_row<1, NW>(T, seed, o);
-  for (uint32_t j = 0; j < pm1; ++j) o[0] = xor4(o[0], and4(K->lastcw[j], 0u - ((t >> j) & 1u)));
-  return o[0];
-}
 
 template <bool FINAL, int NRP>
 __global__ __launch_bounds__(kExpThreads) void k_expand(
@@ -1973,8 +1912,9 @@ __global__ void k_encode_across(const uint8_t* __restrict__ files, uint64_t fpit
 // ------------------------------------------------------------------------------------------
 // host side: tables, plans, launchers
 // ------------------------------------------------------------------------------------------
-TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last) {
+TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last, int p) {
   TreePlan pl{};
+  pl.p = p;
   pl.n = n;
   pl.log_parts = log_parts;
   pl.prefix = prefix;
@@ -2264,12 +2204,23 @@ hipError_t launch_frontier(const TreePlan& pl, const KeySrc& ks, const NodeBufs&
   return hipGetLastError();
 }
 
+bool leaf_dfs_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("PIR_LEAF_DFS");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 template <int NRP>
-static hipError_t launch_stage(const Stage& st, const DevKey* d_key, const uint4* is,
+static hipError_t launch_stage(int p, const Stage& st, const DevKey* d_key, const uint4* is,
                                const uint32_t* it, uint4* os, uint32_t* ot, uint8_t* c,
                                uint32_t cstride, unsigned blocks, int nkeys, uint64_t in_stride,
                                uint64_t out_stride, uint32_t c_key_off, hipStream_t s) {
   const dim3 grid(blocks, nkeys);
+  if (st.final && leaf_dfs_enabled() && leaves_supported(st.k))
+    return launch_leaves(p, NRP, st.k, d_key, is, it, st.L_in, (uint64_t)blocks * st.tile, nkeys,
+                         in_stride, c, cstride, c_key_off, s);
   if (st.final)
     hipLaunchKernelGGL((k_expand<true, NRP>), grid, dim3(kExpThreads), 0, s, d_key, is, it,
                        st.L_in, st.k, st.tile, os, ot, c, cstride, in_stride, out_stride,
@@ -2307,7 +2258,7 @@ hipError_t launch_stages(const TreePlan& pl, const DevKey* d_key, const NodeBufs
     uint8_t* c = d_c ? d_c + o0 * cs : nullptr;
     const unsigned blocks = (unsigned)(nin / st.tile);
     hipError_t e;
-#define PIR_STAGE(N) launch_stage<N>(st, d_key, is, it, os, ot, c, cs, blocks, nkeys, in_stride, stride, c_key_off, s)
+#define PIR_STAGE(N) launch_stage<N>(pl.p >= 2 ? pl.p : 17, st, d_key, is, it, os, ot, c, cs, blocks, nkeys, in_stride, stride, c_key_off, s)
     switch (nrp) {
       case 1: e = PIR_STAGE(1); break;
       case 2: e = PIR_STAGE(2); break;

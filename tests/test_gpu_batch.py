@@ -109,3 +109,43 @@ def test_batch_pir_property_full_size(pir):
     table = np.array([O.gf_mul(int(fcw[0]), x) for x in range(256)], np.uint8)
     for q in range(nk):
         assert np.array_equal(ans[0][q][0] ^ ans[1][q][0], table[recs[q]]), q
+
+
+# ------------------------------------------------------------------ the depth-first leaf stage
+# k_leaves (pir_leaves.hip) takes every leaf-converting stage of 4-5 levels: one input node per
+# lane, 4-table AES with byte-trimmed control-bit (1/2/4 bytes for p = 2-5 / 6-9 / 10-17) and
+# leaf blocks.  Its answers must equal the oracle's for every share width (nrp 1-16), party
+# count class and leaf-stage depth, alone and batched.
+LEAF_SHAPES = [  # (p, n, nq)
+    (2, 16, 1), (3, 17, 2), (5, 15, 4), (8, 16, 5), (9, 14, 8), (12, 15, 9), (17, 14, 16),
+]
+
+
+@pytest.mark.parametrize("shape", LEAF_SHAPES, ids=lambda s: "p%d_n%d_nq%d" % s)
+def test_leaf_stage_eval_all_vs_oracle(pir, shape):
+    p, n, nq = shape
+    rng = np.random.default_rng(hash(shape) & 0xFFFF)
+    idx = int(rng.integers(0, 1 << n))
+    seeds = rng.integers(0, 256, 16 * p, dtype=np.uint8).tobytes()
+    keys = O.gen_keys(n, idx, O.final_cw(p, nq, 1), p, nq, seeds)
+    for party in sorted({0, p - 1}):
+        with pir.Engine(p, party + 1, n, 16, nq) as e:
+            got = e.eval_all(keys[party])
+        assert np.array_equal(got, O.eval_all(p, party, n, keys[party], nq)), party
+
+
+@pytest.mark.parametrize("klast", [4, 5])
+@pytest.mark.parametrize("p,n,efs,nq,nk,g", [(2, 15, 256, 1, 10, 8), (8, 14, 64, 5, 3, 2),
+                                             (12, 13, 32, 9, 2, 1), (3, 14, 48, 2, 9, 0)])
+def test_batch_leaf_depth_vs_oracle(pir, monkeypatch, klast, p, n, efs, nq, nk, g):
+    monkeypatch.setenv("PIR_BATCH_KLAST", str(klast))
+    rng = np.random.default_rng(1000 * klast + p)
+    keys = _keys(p, n, nq, rng.integers(0, 1 << n, nk), rng)
+    shard = rng.integers(0, 256, (1 << n) * efs, dtype=np.uint8)
+    party = p - 1
+    with pir.Engine(p, party + 1, n, efs, nq) as e:
+        e.set_shard(shard)
+        e.batch_group = g
+        got = e.answer_batch([k[party] for k in keys])
+    for q in range(nk):
+        assert np.array_equal(got[q], O.answer(p, party + 1, n, efs, nq, keys[q][party], shard)), q
