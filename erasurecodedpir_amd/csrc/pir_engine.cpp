@@ -397,7 +397,7 @@ int answer_batch_core(pir_engine* e, const uint8_t* d_raw, int nk, int log_parts
   e->last_batch_group = G;
   e->last_fused = 0;
   e->last_chunks = 1;
-  const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix, e->batch_k_last, c.num_parties);
+  const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix, e->batch_k_last, c.num_parties, 8);
   const pir::ScanShape sh =
       pir::make_scan_shape(pl.nleaves, e->pitch, W, e->num_cus, e->batch_scan_bpc);
   const size_t cb_bytes = (size_t)pl.nleaves * W;

@@ -12,6 +12,7 @@ constexpr int kScanThreads = 512;
 constexpr int kScanBlocksPerCU = 2;
 constexpr int kReduceThreads = 1024;
 constexpr int kColGroupLanes = 64;  // one wave's lanes cover a column group of a record
+constexpr int kBufRsrcWord3 = 0x00020000;  // gfx9 raw buffer: 32-bit data format, no swizzle
 
 // One DPF key, parsed for the device (written by k_key_prep from the raw key bytes whose
 // layout is genOptimizedDPF's: dpf_tree.cpp:254-269).
@@ -49,7 +50,10 @@ struct NodeBufs {  // ping-pong node arrays in global memory (max_nodes entries 
 };
 
 // k_last: levels of the leaf-converting last stage (-1: default 4 for k_expand<FINAL>)
-TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last = -1, int p = 0);
+// max_front: levels of the column-shape frontier (16; batched answers 8: their upper levels
+// then run as depth-first node stages of 4 levels, F in [8, 11] so that they divide evenly)
+TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last = -1, int p = 0,
+                   int max_front = 16);
 int final_stage_blocks(const TreePlan& pl);  // workgroups of the leaf-converting stage
 
 void upload_aes_table(hipStream_t s);  // Te0 (computed on the host) -> __constant__ memory
@@ -96,7 +100,15 @@ hipError_t launch_leaves(int p, int nrp, int kd, const DevKey* d_key, const uint
                          const uint32_t* it, int L0, uint64_t nin, int nkeys, uint64_t in_stride,
                          uint8_t* c, uint32_t cstride, uint32_t c_key_off, hipStream_t s);
 void upload_leaves_aes_table(hipStream_t s);
-// $PIR_LEAF_DFS=0: final stages on k_expand<FINAL> (breadth first) instead of k_leaves
+// The node-writing stages of kd in [1, kNodesMaxK] levels the same way (one input node per
+// lane, its 2^kd descendants of the stage's last level written to os/ot, out_stride per key).
+constexpr int kNodesMaxK = 4;
+bool nodes_dfs_supported(int kd);
+hipError_t launch_nodes_dfs(int p, int kd, const DevKey* d_key, const uint4* is,
+                            const uint32_t* it, int L0, uint64_t nin, int nkeys,
+                            uint64_t in_stride, uint4* os, uint32_t* ot, uint64_t out_stride,
+                            hipStream_t s);
+// $PIR_LEAF_DFS=0: every stage on k_expand (breadth first in LDS) instead of k_subtree
 bool leaf_dfs_enabled();
 // scan rows [0, nrec) of `shard` (row pitch `pitch`) with coefficients cT[i*nrp + a]
 struct ScanShape {
@@ -106,7 +118,14 @@ struct ScanShape {
   uint32_t slab_bytes;   // per-workgroup partial = nq * 64 * vec * 4
   dim3 grid;
   int threads;           // k_scan_uni workgroup: kScanThreads, or kScanM4rThreads (4-5 rounds)
+  bool tfold;            // k_scan_t (pir_scan_t.hip): transposed four-Russians fold, VEC = 1
 };
+// k_scan_t takes 4-8 rounds of 4/8 coefficient bytes per record over records of >= 256 B
+// ($PIR_SCAN_T=0: the k_scan_uni forms instead)
+bool scan_t_enabled();
+bool scan_t_shape(int nq, int nrp, uint32_t pitch);
+hipError_t launch_scan_t(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
+                         const uint8_t* d_c, uint8_t* d_slabs, int acc, hipStream_t s);
 // k_scan_uni for 4-5 rounds at two dwords per lane: four-Russians folds need 168 VGPRs, so one
 // 768-thread workgroup per CU (only where the caller leaves the CU to the scan: blocks_per_cu 0)
 constexpr int kScanM4rThreads = 768;

@@ -387,7 +387,6 @@ __device__ __forceinline__ Chunk<VEC> load_chunk_buf(__amdgpu_buffer_rsrc_t r, u
   }
   return ch;
 }
-constexpr int kBufRsrcWord3 = 0x00020000;  // gfx9 raw buffer: 32-bit data format, no swizzle
 
 // Four-Russians plane indices of a group of 4 rows (pir_m4r.h): lane k = plane (k / 8, k % 8)
 // takes bit k % 8 of the rows' round-k/8 coefficient bytes -- bit k of each row's 64-bit
@@ -1912,7 +1911,7 @@ __global__ void k_encode_across(const uint8_t* __restrict__ files, uint64_t fpit
 // ------------------------------------------------------------------------------------------
 // host side: tables, plans, launchers
 // ------------------------------------------------------------------------------------------
-TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last, int p) {
+TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last, int p, int max_front) {
   TreePlan pl{};
   pl.p = p;
   pl.n = n;
@@ -1925,7 +1924,9 @@ TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last, int p) {
   if (k_last < 0) k_last = 4;
   k_last = std::min(k_last, nr);
   const int L_last = nr - k_last;
-  const int F = std::min(16, L_last);
+  int F = std::min(16, L_last);
+  if (max_front < 16 && leaf_dfs_enabled())
+    F = L_last <= max_front ? L_last : max_front + (L_last - max_front) % 4;
   pl.F = F;
   pl.g = std::min(F, 8);
   pl.e = F - pl.g;
@@ -2221,6 +2222,10 @@ static hipError_t launch_stage(int p, const Stage& st, const DevKey* d_key, cons
   if (st.final && leaf_dfs_enabled() && leaves_supported(st.k))
     return launch_leaves(p, NRP, st.k, d_key, is, it, st.L_in, (uint64_t)blocks * st.tile, nkeys,
                          in_stride, c, cstride, c_key_off, s);
+  if (!st.final && leaf_dfs_enabled() && nodes_dfs_supported(st.k) &&
+      (uint64_t)blocks * st.tile * nkeys >= (1u << 18))  // >= 256 workgroups of one node per lane
+    return launch_nodes_dfs(p, st.k, d_key, is, it, st.L_in, (uint64_t)blocks * st.tile, nkeys,
+                            in_stride, os, ot, out_stride, s);
   if (st.final)
     hipLaunchKernelGGL((k_expand<true, NRP>), grid, dim3(kExpThreads), 0, s, d_key, is, it,
                        st.L_in, st.k, st.tile, os, ot, c, cstride, in_stride, out_stride,
@@ -2295,6 +2300,8 @@ ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus, in
   else if (nq == 3 && sh.vec == 4 && pitch / 8 < (uint32_t)kColGroupLanes &&
            pitch / 4 >= (uint32_t)kColGroupLanes)
     sh.vec = 1;  // 3 rounds, 256-511 B: a record per wave row at VEC = 1
+  sh.tfold = scan_t_shape(nq, sh.nrp, pitch);
+  if (sh.tfold) sh.vec = 1;  // the transposed fold: one dword per lane, any record width
   sh.pitch = pitch;
   sh.cpr = pitch / (sh.vec * 4);
   sh.uniform = sh.cpr >= (uint32_t)kColGroupLanes;
@@ -2307,13 +2314,20 @@ ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus, in
   uint64_t gx = std::max<uint64_t>(1, std::min<uint64_t>(want_blocks / gy, (groups + 4 * waves_per_block - 1) / (4 * waves_per_block)));
   sh.grid = dim3((unsigned)gx, gy);
   sh.threads = kScanThreads;
-  if (blocks_per_cu <= 0 && sh.uniform && sh.vec == 2 && (nq == 4 || nq == 5) &&
+  if (!sh.tfold && blocks_per_cu <= 0 && sh.uniform && sh.vec == 2 && (nq == 4 || nq == 5) &&
       !(getenv("PIR_SCAN_M4R") && atoi(getenv("PIR_SCAN_M4R")) == 0)) {
     // the four-Russians k_scan_uni: one 768-thread workgroup per CU and column group
     const uint64_t wpb = kScanM4rThreads / 64;
     gx = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)num_cus / gy, (groups + 4 * wpb - 1) / (4 * wpb)));
     sh.grid = dim3((unsigned)gx, gy);
     sh.threads = kScanM4rThreads;
+  }
+  // k_scan_t addresses a wave's rows through one buffer resource: < 2^31 bytes of rows per wave
+  // (only shards of tens of GiB with wide records reach it)
+  if (sh.tfold) {
+    const uint64_t wpb = (uint64_t)sh.threads / 64;
+    while ((groups / (sh.grid.x * wpb) + 1) * pitch >= (1ull << 31) && sh.grid.x < (1u << 30))
+      sh.grid.x *= 2;
   }
   sh.slab_bytes = (uint32_t)(nq * kColGroupLanes * sh.vec * 4);
   return sh;
@@ -2361,6 +2375,7 @@ static hipError_t scan_nq(const ScanShape& sh, const uint8_t* d_shard, uint64_t 
 hipError_t launch_scan(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
                        const uint8_t* d_c, uint8_t* d_slabs, bool accumulate, hipStream_t s) {
   const int acc = accumulate ? 1 : 0;
+  if (sh.tfold) return launch_scan_t(sh, d_shard, nrec, d_c, d_slabs, acc, s);
   switch (sh.nq) {
     case 1: return scan_nq<1>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
     case 2: return scan_nq<2>(sh, d_shard, nrec, d_c, d_slabs, acc, s);

@@ -1,14 +1,17 @@
-// pir_leaves.hip -- the leaf-converting last stage of the DPF tree, depth first per lane.
+// pir_leaves.hip -- the throughput stages of the DPF tree, depth first per lane (k_subtree).
 //
 // k_expand builds a stage breadth first in LDS: a workgroup of 1024 threads starts from `tile`
 // nodes, so its first levels keep only 4 and 8 of its 16 waves busy (256 and 512 nodes) and
 // every level ends at a barrier.  Here every lane owns ONE input node of level L0 and walks its
 // subtree of 2^KD leaves depth first in registers (the pending right child of each level waits
 // in 5 VGPRs), so all waves are busy from the first level, there is no node traffic through
-// LDS and no barrier after the table fill.  The work is the reference's (dpf_tree.cpp:525-580):
-// KD levels of G(seed) expansions + correction words, then the leaf conversion
-//   c[leaf][a] = AES_{s_leaf}(0)[a] ^ XOR_{k: t_leaf bit k} lastCW[k][a]   (a < nq).
-// blockIdx.y = key of a batch (its DevKey, input node range and share slot), as in k_expand.
+// LDS and no barrier after the table fill.  The AES is the 4-table T-box of pir_aes4.h (the
+// kernel holds nothing else in LDS).  The work is the reference's (dpf_tree.cpp:525-580):
+// KD levels of G(seed) expansions + correction words, then either
+//   * leaf stage: the leaf conversion c[leaf][a] = AES_{s_leaf}(0)[a] ^ XOR_{k: t_leaf bit k}
+//     lastCW[k][a] (a < nq), or
+//   * node stage: the 2^KD nodes (seed, control bits) of the stage's last level, for the next.
+// blockIdx.y = key of a batch (its DevKey, input node range and outputs), as in k_expand.
 #include "pir_kernels.h"
 #include "pir_tree.h"
 #include "pir_aes4.h"
@@ -52,102 +55,165 @@ __device__ __forceinline__ uint4 leaf_value4(const Tab4& T, const DevKey* __rest
   return o[0];
 }
 
-// the 2^D leaves under node (s, t) of level L, leaf indices [leaf, leaf + 2^D)
-template <int NRP, int TB, int D>
-__device__ __forceinline__ void leaves_dfs(const Tab4& T, const DevKey* __restrict__ K, int L,
-                                           const Bits& B, uint4 s, uint32_t t,
-                                           uint8_t* __restrict__ c, uint64_t leaf,
-                                           uint32_t cstride, const uint4& qm) {
+// Where a subtree's bottom level goes: the DPF shares of its leaves (leaf stage) or its nodes
+// (seed, control bits) for the next stage (node stage).
+struct DfsOut {
+  uint8_t* c;        // leaf stage: leaf i's NRP share bytes at c + i * cstride
+  uint32_t cstride;
+  uint4 qm;          // ... masked to the nq bytes
+  uint4* s;          // node stage: node i at s[i], t[i]
+  uint32_t* t;
+};
+
+// the 2^D leaves (or bottom nodes) under node (s, t) of level L, indices [i0, i0 + 2^D)
+template <bool NODES, int NRP, int TB, int D>
+__device__ __forceinline__ void subtree_dfs(const Tab4& T, const DevKey* __restrict__ K, int L,
+                                            const Bits& B, uint4 s, uint32_t t, uint64_t i0,
+                                            const DfsOut& o) {
   uint4 sl, sr;
   uint32_t tl, tr;
   expand_node4<TB>(T, K, L, B, s, t, sl, sr, tl, tr);
   if constexpr (D == 1) {
-    const uint4 vl = leaf_value4<NRP>(T, K, B.pm1, sl, tl);
-    const uint4 vr = leaf_value4<NRP>(T, K, B.pm1, sr, tr);
-    store_leaf<NRP>(c, leaf, and_q(vl, qm), cstride);
-    store_leaf<NRP>(c, leaf + 1, and_q(vr, qm), cstride);
+    if constexpr (NODES) {
+      o.s[i0] = sl; o.s[i0 + 1] = sr;
+      o.t[i0] = tl; o.t[i0 + 1] = tr;
+    } else {
+      const uint4 vl = leaf_value4<NRP>(T, K, B.pm1, sl, tl);
+      const uint4 vr = leaf_value4<NRP>(T, K, B.pm1, sr, tr);
+      store_leaf<NRP>(o.c, i0, and_q(vl, o.qm), o.cstride);
+      store_leaf<NRP>(o.c, i0 + 1, and_q(vr, o.qm), o.cstride);
+    }
   } else {
     // one copy of the subtree code per level: the right child waits in registers
 #pragma unroll 1
     for (int i = 0; i < 2; ++i)
-      leaves_dfs<NRP, TB, D - 1>(T, K, L + 1, B, i ? sr : sl, i ? tr : tl, c,
-                                 leaf + ((uint64_t)i << (D - 1)), cstride, qm);
+      subtree_dfs<NODES, NRP, TB, D - 1>(T, K, L + 1, B, i ? sr : sl, i ? tr : tl,
+                                         i0 + ((uint64_t)i << (D - 1)), o);
   }
 }
 
-template <int NRP, int TB, int KD>
+// blockIdx.y = key of a batch: its DevKey, input node range (in_stride apart) and outputs
+// (shares at c + y * c_key_off, or nodes out_stride apart)
+template <bool NODES, int NRP, int TB, int KD>
 __global__ __launch_bounds__(kLeafThreads)
-void k_leaves(const DevKey* __restrict__ K, const uint4* __restrict__ in_s,
-              const uint32_t* __restrict__ in_t, int L0, uint64_t nin, uint64_t in_stride,
-              uint8_t* __restrict__ c, uint32_t cstride, uint32_t c_key_off) {
+void k_subtree(const DevKey* __restrict__ K, const uint4* __restrict__ in_s,
+               const uint32_t* __restrict__ in_t, int L0, uint64_t nin, uint64_t in_stride,
+               uint8_t* __restrict__ c, uint32_t cstride, uint32_t c_key_off,
+               uint4* __restrict__ out_s, uint32_t* __restrict__ out_t, uint64_t out_stride) {
   K += blockIdx.y;
   in_s += blockIdx.y * in_stride;
   in_t += blockIdx.y * in_stride;
-  c += (size_t)blockIdx.y * c_key_off;
   __shared__ uint32_t tab[kTab4Bytes / 4];
   load_tables4_n<kLeafThreads>(tab);
   const Bits B(K->p);
-  uint4 qm;  // keep the nq output bytes
-  {
-    const int nq = (int)K->nq;
+  DfsOut o;
+  if constexpr (NODES) {
+    o.s = out_s + blockIdx.y * out_stride;
+    o.t = out_t + blockIdx.y * out_stride;
+  } else {
+    o.c = c + (size_t)blockIdx.y * c_key_off;
+    o.cstride = cstride;
+    const int nq = (int)K->nq;  // keep the nq output bytes
     uint32_t m[4];
     for (int w = 0; w < 4; ++w) {
       const int nb = nq - 4 * w;
       m[w] = nb >= 4 ? 0xffffffffu : (nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u));
     }
-    qm = make_uint4(m[0], m[1], m[2], m[3]);
+    o.qm = make_uint4(m[0], m[1], m[2], m[3]);
   }
   __syncthreads();
   const Tab4 T(tab);
   const uint64_t u = (uint64_t)blockIdx.x * kLeafThreads + threadIdx.x;
   if (u >= nin) return;  // no barrier below
-  leaves_dfs<NRP, TB, KD>(T, K, L0, B, in_s[u], in_t[u], c, u << KD, cstride, qm);
+  subtree_dfs<NODES, NRP, TB, KD>(T, K, L0, B, in_s[u], in_t[u], u << KD, o);
 }
 
 bool leaves_supported(int kd) { return kd >= kLeavesMinK && kd <= kLeavesMaxK; }
+bool nodes_dfs_supported(int kd) { return kd >= 1 && kd <= kNodesMaxK; }
 
-template <int NRP, int TB>
-static hipError_t leaves_tb(int kd, dim3 grid, const DevKey* d_key, const uint4* is,
-                             const uint32_t* it, int L0, uint64_t nin, uint64_t in_stride,
-                             uint8_t* c, uint32_t cstride, uint32_t c_key_off, hipStream_t s) {
-#define PIR_LV(KD)                                                                            \
-  hipLaunchKernelGGL((k_leaves<NRP, TB, KD>), grid, dim3(kLeafThreads), 0, s, d_key, is, it, L0, \
-                     nin, in_stride, c, cstride, c_key_off)
-  switch (kd) {
-    case 4: PIR_LV(4); break;
-    case 5: PIR_LV(5); break;
-    default: return hipErrorInvalidValue;
-  }
-#undef PIR_LV
+struct SubtreeArgs {
+  const DevKey* key;
+  const uint4* is;
+  const uint32_t* it;
+  int L0;
+  uint64_t nin, in_stride;
+  uint8_t* c;
+  uint32_t cstride, c_key_off;
+  uint4* os;
+  uint32_t* ot;
+  uint64_t out_stride;
+};
+
+template <bool NODES, int NRP, int TB, int KD>
+static hipError_t subtree_launch(dim3 grid, const SubtreeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((k_subtree<NODES, NRP, TB, KD>), grid, dim3(kLeafThreads), 0, s, a.key,
+                     a.is, a.it, a.L0, a.nin, a.in_stride, a.c, a.cstride, a.c_key_off, a.os,
+                     a.ot, a.out_stride);
   return hipGetLastError();
 }
 
 // TB = bytes of the control-bit block the node reads: 2(p-1) bits
+template <int NRP, int TB>
+static hipError_t leaves_kd(int kd, dim3 grid, const SubtreeArgs& a, hipStream_t s) {
+  switch (kd) {
+    case 4: return subtree_launch<false, NRP, TB, 4>(grid, a, s);
+    case 5: return subtree_launch<false, NRP, TB, 5>(grid, a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
 template <int NRP>
-static hipError_t leaves_nrp(int p, int kd, dim3 grid, const DevKey* d_key, const uint4* is,
-                             const uint32_t* it, int L0, uint64_t nin, uint64_t in_stride,
-                             uint8_t* c, uint32_t cstride, uint32_t c_key_off, hipStream_t s) {
+static hipError_t leaves_nrp(int p, int kd, dim3 grid, const SubtreeArgs& a, hipStream_t s) {
   const int tbits = 2 * (p - 1);
-  if (tbits <= 8) return leaves_tb<NRP, 1>(kd, grid, d_key, is, it, L0, nin, in_stride, c, cstride, c_key_off, s);
-  if (tbits <= 16) return leaves_tb<NRP, 2>(kd, grid, d_key, is, it, L0, nin, in_stride, c, cstride, c_key_off, s);
-  return leaves_tb<NRP, 4>(kd, grid, d_key, is, it, L0, nin, in_stride, c, cstride, c_key_off, s);
+  if (tbits <= 8) return leaves_kd<NRP, 1>(kd, grid, a, s);
+  if (tbits <= 16) return leaves_kd<NRP, 2>(kd, grid, a, s);
+  return leaves_kd<NRP, 4>(kd, grid, a, s);
+}
+template <int TB>
+static hipError_t nodes_kd(int kd, dim3 grid, const SubtreeArgs& a, hipStream_t s) {
+  switch (kd) {
+    case 1: return subtree_launch<true, 1, TB, 1>(grid, a, s);
+    case 2: return subtree_launch<true, 1, TB, 2>(grid, a, s);
+    case 3: return subtree_launch<true, 1, TB, 3>(grid, a, s);
+    case 4: return subtree_launch<true, 1, TB, 4>(grid, a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+static bool subtree_grid(uint64_t nin, int nkeys, int p, dim3& grid) {
+  if (nkeys < 1 || nin == 0 || p < 2 || p > 17) return false;
+  const uint64_t blocks = (nin + kLeafThreads - 1) / kLeafThreads;
+  if (blocks > 0x7fffffffull || nkeys > 65535) return false;
+  grid = dim3((unsigned)blocks, (unsigned)nkeys);
+  return true;
 }
 
 hipError_t launch_leaves(int p, int nrp, int kd, const DevKey* d_key, const uint4* is,
                          const uint32_t* it, int L0, uint64_t nin, int nkeys, uint64_t in_stride,
                          uint8_t* c, uint32_t cstride, uint32_t c_key_off, hipStream_t s) {
-  if (!leaves_supported(kd) || nkeys < 1 || nin == 0 || p < 2 || p > 17) return hipErrorInvalidValue;
-  const uint64_t blocks = (nin + kLeafThreads - 1) / kLeafThreads;
-  if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)blocks, (unsigned)nkeys);
+  dim3 grid;
+  if (!leaves_supported(kd) || !subtree_grid(nin, nkeys, p, grid)) return hipErrorInvalidValue;
+  const SubtreeArgs a{d_key, is, it, L0, nin, in_stride, c, cstride, c_key_off, nullptr, nullptr, 0};
   switch (nrp) {
-    case 1: return leaves_nrp<1>(p, kd, grid, d_key, is, it, L0, nin, in_stride, c, cstride, c_key_off, s);
-    case 2: return leaves_nrp<2>(p, kd, grid, d_key, is, it, L0, nin, in_stride, c, cstride, c_key_off, s);
-    case 4: return leaves_nrp<4>(p, kd, grid, d_key, is, it, L0, nin, in_stride, c, cstride, c_key_off, s);
-    case 8: return leaves_nrp<8>(p, kd, grid, d_key, is, it, L0, nin, in_stride, c, cstride, c_key_off, s);
-    case 16: return leaves_nrp<16>(p, kd, grid, d_key, is, it, L0, nin, in_stride, c, cstride, c_key_off, s);
+    case 1: return leaves_nrp<1>(p, kd, grid, a, s);
+    case 2: return leaves_nrp<2>(p, kd, grid, a, s);
+    case 4: return leaves_nrp<4>(p, kd, grid, a, s);
+    case 8: return leaves_nrp<8>(p, kd, grid, a, s);
+    case 16: return leaves_nrp<16>(p, kd, grid, a, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_nodes_dfs(int p, int kd, const DevKey* d_key, const uint4* is,
+                            const uint32_t* it, int L0, uint64_t nin, int nkeys,
+                            uint64_t in_stride, uint4* os, uint32_t* ot, uint64_t out_stride,
+                            hipStream_t s) {
+  dim3 grid;
+  if (!nodes_dfs_supported(kd) || !subtree_grid(nin, nkeys, p, grid)) return hipErrorInvalidValue;
+  const SubtreeArgs a{d_key, is, it, L0, nin, in_stride, nullptr, 0, 0, os, ot, out_stride};
+  const int tbits = 2 * (p - 1);
+  if (tbits <= 8) return nodes_kd<1>(kd, grid, a, s);
+  if (tbits <= 16) return nodes_kd<2>(kd, grid, a, s);
+  return nodes_kd<4>(kd, grid, a, s);
 }
 
 }  // namespace pir

@@ -1,0 +1,203 @@
+// pir_scan_t.hip -- the many-round GF(2^8) scan as a transposed four-Russians fold (k_scan_t).
+//
+// The answer of round a is ans_a = sum_i c_a[i] * x_i over GF(2^8) (server.cpp:121-127).  Over
+// bit planes (coding.cpp:9-21, poly 0x11d): ans_a = sum_b alpha^b Z_{a,b}, Z_{a,b} = XOR of the
+// rows whose round-a coefficient has bit b set.  With one record per wave row the coefficient
+// word w_i (the record's NRP <= 8 coefficient bytes, round a = byte a, as 64 bits: plane
+// p = 8a + b) is wave-uniform, and the scans of pir_kernels.hip select each plane's row
+// combination by GPR index (pir_m4r.h): one index switch per plane per 4 rows, whose cost grows
+// with the number of planes (2.2 TB/s at 64 planes, 3.4 at 40: profiles/r02_micro/).
+//
+// Here the roles are swapped.  Per lane and 8 rows, bit j of the lane's 8 row dwords forms an
+// 8-bit index n_j (an 8 x 32 bit transpose of the rows, pir_bits.h), and the wave keeps in LDS a
+// table of the 256 XOR combinations of the 8 rows' coefficient words, T[v] = XOR_{r: bit r of v}
+// w_r.  Then for every bit position j: Zt[j] ^= T[n_j] -- one ds_read_b64 and two v_xor --
+// where Zt[j] (64 bits) is bit j of the lane's dword in every plane at once.  The cost per row
+// no longer depends on the number of planes (up to 64), and no scalar index setting is left in
+// the loop.  At the end Zt is transposed back to planes (32 x 32 bit transposes) and folded by
+// the alpha powers as in k_scan_uni; slabs and k_reduce are unchanged.
+//
+// One record per wave row at one dword per lane (pitch >= 256 B; column groups of 64 dwords
+// along grid y), NRP = 4 or 8 coefficient bytes per record (NQ <= NRP rounds), rows of a wave
+// through one buffer resource with the row offset in soffset (< 2^31 B of rows per wave: host).
+#include "pir_bits.h"
+#include "pir_kernels.h"
+
+namespace pir {
+
+constexpr int kScanTThreads = 512;
+constexpr int kScanTWaves = kScanTThreads / 64;
+
+__device__ __forceinline__ uint32_t gf_xtime4_t(uint32_t x) {  // 4 packed bytes times alpha
+  return ((x & 0x7f7f7f7fu) << 1) ^ (((x >> 7) & 0x01010101u) * 0x1du);
+}
+
+template <int NQ, int NRP>
+__global__ __launch_bounds__(kScanTThreads) __attribute__((amdgpu_waves_per_eu(4)))
+void k_scan_t(const uint8_t* __restrict__ shard, uint64_t nrec, uint32_t pitch, uint32_t cpr,
+              const uint8_t* __restrict__ c, uint8_t* __restrict__ slabs, int accumulate) {
+  static_assert(NRP == 4 || NRP == 8, "coefficient words of 32 or 64 bits");
+  static_assert(NQ >= 1 && NQ <= NRP, "rounds");
+  constexpr int WD = NRP / 4;  // coefficient words per record (rounds 0-3, 4-7)
+  constexpr int GW = kColGroupLanes;
+  __shared__ uint32_t tab[kScanTWaves][256 * WD];  // per wave: T[v] at [v * WD]
+  __shared__ uint32_t red[NQ * GW];
+  for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) red[i] = 0;
+
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t wave = (uint64_t)blockIdx.x * kScanTWaves + wv;
+  const uint64_t nwaves = (uint64_t)gridDim.x * kScanTWaves;
+  const uint32_t chunk = blockIdx.y * kColGroupLanes + lane;
+  const bool active = chunk < cpr;
+  const uint64_t r0 = wave * nrec / nwaves, r1 = (wave + 1) * nrec / nwaves;
+  uint32_t* const tw = &tab[wv][0];
+
+  uint32_t Zt[32][WD];
+#pragma unroll
+  for (int j = 0; j < 32; ++j)
+#pragma unroll
+    for (int d = 0; d < WD; ++d) Zt[j][d] = 0;
+
+  if (r1 > r0) {
+    const uint32_t nrows = (uint32_t)(r1 - r0);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(shard + r0 * pitch), (short)0, (int)(nrows * pitch), kBufRsrcWord3);
+    const uint32_t voff = (active ? chunk : 0u) * 4u;  // inactive lanes: the row's first dword
+    // rows past the wave's last re-read row r0 and have zero coefficient words
+    auto load_rel = [&](uint32_t rel) __attribute__((always_inline)) {
+      return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, voff, rel < nrows ? rel * pitch : 0u, 2);
+    };
+    // lane l: the coefficient words of row rb + l (zero past the wave's rows)
+    auto coefs64 = [&](uint32_t rb) __attribute__((always_inline)) {
+      const uint32_t rl = rb + lane;
+      uint2 cw = make_uint2(0, 0);
+      if (rl < nrows) {
+        const uint8_t* p = c + (r0 + rl) * NRP;
+        if constexpr (NRP == 8) cw = *reinterpret_cast<const uint2*>(p);
+        else cw.x = *reinterpret_cast<const uint32_t*>(p);
+      }
+      return cw;
+    };
+    // table entries lane + 64 k: the XOR of w_r over the set bits r < 6 of the lane, then w6, w7
+    uint32_t lm[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) lm[r] = ((lane >> r) & 1u) ? 0xffffffffu : 0u;
+
+    uint32_t x[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) x[u] = load_rel((uint32_t)u);
+    uint2 cw = coefs64(0);
+    for (uint32_t rb = 0; rb < nrows; rb += 64) {
+      const uint2 cwn = coefs64(rb + 64);  // the next 64 rows' coefficient words, in flight
+      const uint32_t nb = nrows - rb < 64 ? nrows - rb : 64;
+      for (uint32_t j0 = 0; j0 < nb; j0 += 16) {
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const uint32_t j = j0 + 8 * g;
+          // ---- the wave's table of the 8 rows' coefficient combinations
+#pragma unroll
+          for (int d = 0; d < WD; ++d) {
+            uint32_t w[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+              w[r] = (uint32_t)__builtin_amdgcn_readlane((int)(d ? cw.y : cw.x), (int)(j + r));
+            uint32_t e = 0;
+#pragma unroll
+            for (int r = 0; r < 6; ++r) e = __builtin_amdgcn_bitop3_b32(e, w[r], lm[r], 0x78);
+            const uint32_t e6 = e ^ w[6], e7 = e ^ w[7];
+            tw[lane * WD + d] = e;
+            tw[(lane + 64) * WD + d] = e6;
+            tw[(lane + 128) * WD + d] = e7;
+            tw[(lane + 192) * WD + d] = e6 ^ w[7];
+          }
+          __builtin_amdgcn_wave_barrier();  // the wave's own table: LDS keeps its order
+          // ---- bit j of the 8 rows -> index byte; one lookup per bit position
+          uint32_t (&R)[8] = *reinterpret_cast<uint32_t(*)[8]>(&x[8 * g]);  // in place
+          transpose8x32(R);
+#pragma unroll
+          for (int jj = 0; jj < 32; ++jj) {
+            const uint32_t idx = (R[jj & 7] >> (8 * (jj >> 3))) & 0xffu;
+            if constexpr (WD == 2) {
+              const uint2 t = *reinterpret_cast<const uint2*>(tw + 2 * idx);
+              Zt[jj][0] ^= t.x;
+              Zt[jj][1] ^= t.y;
+            } else {
+              Zt[jj][0] ^= tw[idx];
+            }
+          }
+          __builtin_amdgcn_wave_barrier();  // reads done before the next group's table
+#pragma unroll
+          for (int r = 0; r < 8; ++r) x[8 * g + r] = load_rel(rb + j + 16 + r);
+          __builtin_amdgcn_sched_barrier(0);  // one group at a time (register pressure)
+        }
+      }
+      cw = cwn;
+    }
+  }
+  __syncthreads();  // red[] zeroed
+  if (active) {
+#pragma unroll
+    for (int d = 0; d < WD; ++d) {
+      if (4 * d >= NQ) continue;
+      uint32_t Y[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) Y[j] = Zt[j][d];
+      transpose32(Y);  // Y[q]: plane 32 d + q = (round 4 d + q / 8, bit q % 8)
+#pragma unroll
+      for (int a4 = 0; a4 < 4; ++a4) {
+        const int a = 4 * d + a4;
+        if (a >= NQ) continue;
+        uint32_t acc = Y[8 * a4 + 7];
+#pragma unroll
+        for (int b = 6; b >= 0; --b) acc = gf_xtime4_t(acc) ^ Y[8 * a4 + b];
+        if (acc) atomicXor(&red[a * GW + lane], acc);
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t* slab = reinterpret_cast<uint32_t*>(slabs) +
+                   ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * (NQ * GW);
+  if (accumulate)
+    for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) slab[i] ^= red[i];
+  else
+    for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) slab[i] = red[i];
+}
+
+bool scan_t_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("PIR_SCAN_T");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+// 6-8 rounds (64 and 48 planes: 3.9 TB/s against 2.2 for the GPR-index fold at configs[2]'s
+// 8); 4-5 rounds only for records narrower than a VEC = 2 wave row (the 768-thread GPR-index
+// k_scan_uni at two dwords per lane is faster there: Hollanti 5 rounds at 1 KiB 4.53 against
+// 4.91 ms, profiles/r03_bench_ch5_*.json)
+bool scan_t_shape(int nq, int nrp, uint32_t pitch) {
+  if (!scan_t_enabled() || nq < 4 || nq > 8 || nq > nrp || (nrp != 4 && nrp != 8)) return false;
+  if (pitch % 4 != 0 || pitch / 4 < (uint32_t)kColGroupLanes) return false;
+  return nq >= 6 || pitch / 8 < (uint32_t)kColGroupLanes;
+}
+
+template <int NQ, int NRP>
+static hipError_t scan_t_launch(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
+                                const uint8_t* d_c, uint8_t* d_slabs, int acc, hipStream_t s) {
+  hipLaunchKernelGGL((k_scan_t<NQ, NRP>), sh.grid, dim3(kScanTThreads), 0, s, d_shard, nrec,
+                     sh.pitch, sh.cpr, d_c, d_slabs, acc);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan_t(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
+                         const uint8_t* d_c, uint8_t* d_slabs, int acc, hipStream_t s) {
+  if (sh.threads != kScanTThreads || sh.vec != 1 || !sh.uniform) return hipErrorInvalidValue;
+#define PIR_ST(NQ, NRP) \
+  if (sh.nq == NQ && sh.nrp == NRP) return scan_t_launch<NQ, NRP>(sh, d_shard, nrec, d_c, d_slabs, acc, s)
+  PIR_ST(4, 4); PIR_ST(4, 8); PIR_ST(5, 8); PIR_ST(6, 8); PIR_ST(7, 8); PIR_ST(8, 8);
+#undef PIR_ST
+  return hipErrorInvalidValue;
+}
+
+}  // namespace pir
