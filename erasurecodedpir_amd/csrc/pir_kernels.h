@@ -121,7 +121,17 @@ struct ScanShape {
   bool tfold;            // k_scan_t (pir_scan_t.hip): transposed four-Russians fold, VEC = 1
 };
 // k_scan_t takes 4-8 rounds of 4/8 coefficient bytes per record over records of >= 256 B
-// ($PIR_SCAN_T=0: the k_scan_uni forms instead)
+// ($PIR_SCAN_T=0: the k_scan_uni forms instead).  Workgroups of kScanTThreads, kScanTBlocksPerCU
+// per CU, kScanTWavesPerEU waves per SIMD (its register budget: 512 / waves VGPRs)
+#ifndef PIR_SCAN_T_THREADS
+#define PIR_SCAN_T_THREADS 256
+#endif
+#ifndef PIR_SCAN_T_WPE
+#define PIR_SCAN_T_WPE 4
+#endif
+constexpr int kScanTThreads = PIR_SCAN_T_THREADS;
+constexpr int kScanTWavesPerEU = PIR_SCAN_T_WPE;
+constexpr int kScanTBlocksPerCU = kScanTWavesPerEU * 4 * 64 / kScanTThreads;
 bool scan_t_enabled();
 bool scan_t_shape(int nq, int nrp, uint32_t pitch);
 hipError_t launch_scan_t(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,

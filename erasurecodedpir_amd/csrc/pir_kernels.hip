@@ -2322,12 +2322,17 @@ ScanShape make_scan_shape(uint64_t nrec, uint32_t pitch, int nq, int num_cus, in
     sh.grid = dim3((unsigned)gx, gy);
     sh.threads = kScanM4rThreads;
   }
-  // k_scan_t addresses a wave's rows through one buffer resource: < 2^31 bytes of rows per wave
-  // (only shards of tens of GiB with wide records reach it)
+  // k_scan_t: its own workgroup size and blocks per CU; it addresses a wave's rows through one
+  // buffer resource, < 2^31 bytes of rows per wave (only shards of tens of GiB reach it)
   if (sh.tfold) {
-    const uint64_t wpb = (uint64_t)sh.threads / 64;
-    while ((groups / (sh.grid.x * wpb) + 1) * pitch >= (1ull << 31) && sh.grid.x < (1u << 30))
-      sh.grid.x *= 2;
+    const uint64_t wpb = kScanTThreads / 64;
+    int bpc = kScanTBlocksPerCU;
+    if (const char* v = getenv("PIR_SCAN_T_BPC")) bpc = std::max(1, std::min(kScanTBlocksPerCU, atoi(v)));
+    const uint64_t want = (uint64_t)num_cus * bpc;  // ($PIR_SCAN_T_BPC: diagnostics)
+    uint64_t gxt = std::max<uint64_t>(1, std::min<uint64_t>(want / gy, (groups + 4 * wpb - 1) / (4 * wpb)));
+    while ((groups / (gxt * wpb) + 1) * pitch >= (1ull << 31) && gxt < (1u << 30)) gxt *= 2;
+    sh.grid = dim3((unsigned)gxt, gy);
+    sh.threads = kScanTThreads;
   }
   sh.slab_bytes = (uint32_t)(nq * kColGroupLanes * sh.vec * 4);
   return sh;

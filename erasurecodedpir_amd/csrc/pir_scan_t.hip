@@ -21,11 +21,12 @@
 // along grid y), NRP = 4 or 8 coefficient bytes per record (NQ <= NRP rounds), rows of a wave
 // through one buffer resource with the row offset in soffset (< 2^31 B of rows per wave: host).
 #include "pir_bits.h"
+#include <stdlib.h>
+#include <type_traits>
 #include "pir_kernels.h"
 
 namespace pir {
 
-constexpr int kScanTThreads = 512;
 constexpr int kScanTWaves = kScanTThreads / 64;
 
 __device__ __forceinline__ uint32_t gf_xtime4_t(uint32_t x) {  // 4 packed bytes times alpha
@@ -33,7 +34,7 @@ __device__ __forceinline__ uint32_t gf_xtime4_t(uint32_t x) {  // 4 packed bytes
 }
 
 template <int NQ, int NRP>
-__global__ __launch_bounds__(kScanTThreads) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(kScanTThreads) __attribute__((amdgpu_waves_per_eu(kScanTWavesPerEU)))
 void k_scan_t(const uint8_t* __restrict__ shard, uint64_t nrec, uint32_t pitch, uint32_t cpr,
               const uint8_t* __restrict__ c, uint8_t* __restrict__ slabs, int accumulate) {
   static_assert(NRP == 4 || NRP == 8, "coefficient words of 32 or 64 bits");
@@ -115,17 +116,39 @@ void k_scan_t(const uint8_t* __restrict__ shard, uint64_t nrec, uint32_t pitch, 
           // ---- bit j of the 8 rows -> index byte; one lookup per bit position
           uint32_t (&R)[8] = *reinterpret_cast<uint32_t(*)[8]>(&x[8 * g]);  // in place
           transpose8x32(R);
+          uint32_t id[32];
 #pragma unroll
-          for (int jj = 0; jj < 32; ++jj) {
-            const uint32_t idx = (R[jj & 7] >> (8 * (jj >> 3))) & 0xffu;
-            if constexpr (WD == 2) {
-              const uint2 t = *reinterpret_cast<const uint2*>(tw + 2 * idx);
-              Zt[jj][0] ^= t.x;
-              Zt[jj][1] ^= t.y;
-            } else {
-              Zt[jj][0] ^= tw[idx];
+          for (int jj = 0; jj < 32; ++jj) id[jj] = (R[jj & 7] >> (8 * (jj >> 3))) & 0xffu;
+          // 4 chunks of 8 lookups, software-pipelined: chunk c + 1's reads are issued before
+          // chunk c's XORs (16 reads in flight; left alone the scheduler waits on each read)
+          using Ent = typename std::conditional<WD == 2, uint2, uint32_t>::type;
+          const Ent* te = reinterpret_cast<const Ent*>(tw);
+          Ent ta[8], tb[8];
+          auto issue = [&](Ent (&t)[8], int ch) __attribute__((always_inline)) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) t[q] = te[id[8 * ch + q]];
+            __builtin_amdgcn_sched_barrier(0);
+          };
+          auto fold = [&](const Ent (&t)[8], int ch) __attribute__((always_inline)) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              if constexpr (WD == 2) {
+                Zt[8 * ch + q][0] ^= t[q].x;
+                Zt[8 * ch + q][1] ^= t[q].y;
+              } else {
+                Zt[8 * ch + q][0] ^= t[q];
+              }
             }
-          }
+            __builtin_amdgcn_sched_barrier(0);
+          };
+          issue(ta, 0);
+          issue(tb, 1);
+          fold(ta, 0);
+          issue(ta, 2);
+          fold(tb, 1);
+          issue(tb, 3);
+          fold(ta, 2);
+          fold(tb, 3);
           __builtin_amdgcn_wave_barrier();  // reads done before the next group's table
 #pragma unroll
           for (int r = 0; r < 8; ++r) x[8 * g + r] = load_rel(rb + j + 16 + r);
@@ -164,13 +187,15 @@ void k_scan_t(const uint8_t* __restrict__ shard, uint64_t nrec, uint32_t pitch, 
     for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) slab[i] = red[i];
 }
 
-bool scan_t_enabled() {
-  static const bool on = [] {
+// $PIR_SCAN_T: 0 = never, 2 = every 4-8 round shape it can take (diagnostics), else the default
+static int scan_t_mode() {
+  static const int mode = [] {
     const char* v = getenv("PIR_SCAN_T");
-    return !(v && v[0] == '0');
+    return v ? atoi(v) : 1;
   }();
-  return on;
+  return mode;
 }
+bool scan_t_enabled() { return scan_t_mode() != 0; }
 
 // 6-8 rounds (64 and 48 planes: 3.9 TB/s against 2.2 for the GPR-index fold at configs[2]'s
 // 8); 4-5 rounds only for records narrower than a VEC = 2 wave row (the 768-thread GPR-index
@@ -179,7 +204,7 @@ bool scan_t_enabled() {
 bool scan_t_shape(int nq, int nrp, uint32_t pitch) {
   if (!scan_t_enabled() || nq < 4 || nq > 8 || nq > nrp || (nrp != 4 && nrp != 8)) return false;
   if (pitch % 4 != 0 || pitch / 4 < (uint32_t)kColGroupLanes) return false;
-  return nq >= 6 || pitch / 8 < (uint32_t)kColGroupLanes;
+  return nq >= 6 || pitch / 8 < (uint32_t)kColGroupLanes || scan_t_mode() == 2;
 }
 
 template <int NQ, int NRP>
