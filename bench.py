@@ -623,6 +623,14 @@ def main():
         if config != "c4":
             out["c4_single_engine"] = extra_leg(ctx, pir, "c4", min(W, 2), min(K, 8), rng,
                                                 single=False)
+        if config != "c5":
+            out["configs4_c5"] = extra_leg(ctx, pir, "c5", min(W, 2), min(K, 10), rng,
+                                           single=False)
+        b = measure_batch(min(K, 3), min(W, 1), ctx, "c3b")
+        out["configs2_c3b"] = {k: b[k] for k in ("value", "unit", "value_kind", "steps", "warmup",
+                                                 "ms_per_step", "ms_per_key", "keys_per_s",
+                                                 "shard_passes_per_step", "parity")}
+        out["configs2_c3b"]["workload"] = b["config"]["workload"]
     if cpu_path:
         try:
             cores = _host_cores() if args.cpu_cores < 0 else args.cpu_cores
@@ -812,6 +820,15 @@ def run_batch(args, ctx, config):
     """A step = `batch` keys answered against the device-resident shard (answer_batch_dev: one
     shard pass per group of keys, one DPF tree per key).  value = effective GiB/s = keys x
     logical shard bytes / time (every key's answer covers the whole shard)."""
+    out = measure_batch(args.steps, args.warmup, ctx, config)
+    if ctx.rank == 0:
+        print(json.dumps(out), flush=True)
+    if ctx.world > 1:
+        ctx.dist.barrier()
+        ctx.dist.destroy_process_group()
+
+
+def measure_batch(steps, warmup, ctx, config):
     import erasurecodedpir_amd as pir
     from erasurecodedpir_amd.dist import broadcast_bytes, log2_exact
 
@@ -831,12 +848,12 @@ def run_batch(args, ctx, config):
     d_keys = eng.alloc_dev(eng.key_len * nk)
     d_res = eng.alloc_dev(eng.answer_bytes * nk)
     eng.h2d(d_keys, b"".join(ks[0] for _, ks in keyset))
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         eng.answer_batch_dev(d_keys, nk, d_res)
-    eng.set_profiling(max(1, args.steps))
-    dt = ctx.timed(eng, lambda: [eng.answer_batch_dev(d_keys, nk, d_res) for _ in range(args.steps)])
+    eng.set_profiling(max(1, steps))
+    dt = ctx.timed(eng, lambda: [eng.answer_batch_dev(d_keys, nk, d_res) for _ in range(steps)])
     eng.set_profiling(0)
-    ms = dt / args.steps * 1e3
+    ms = dt / steps * 1e3
     alone = eng.profile_phases(d_keys, 5)
     got = eng.d2h(d_res, eng.answer_bytes * nk).reshape(nk, nq, efs)
     # correctness at full size: party-1 batch ^ party-2 batch == finalCW * record, every key
@@ -857,7 +874,7 @@ def run_batch(args, ctx, config):
         "value": round(nk * shard_bytes / GIB / (ms / 1e3), 3),
         "unit": "GiB/s",
         "value_kind": "effective: keys x logical shard bytes / batch time",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "n_gpus": world, "steps": steps, "warmup": warmup,
         "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": workload, "records": 1 << n, "record_bytes": efs, "parties": p,
@@ -871,11 +888,7 @@ def run_batch(args, ctx, config):
         "parity": {"pir_record_recovered_all_keys": ok},
     }
     eng.close()
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        ctx.dist.barrier()
-        ctx.dist.destroy_process_group()
+    return out
 
 
 def broadcast_from(arr, src, nbytes):
