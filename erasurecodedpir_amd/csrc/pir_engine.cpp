@@ -145,10 +145,13 @@ struct pir_engine {
   size_t qscratch_cap = 0;
   uint32_t* d_qcnt = nullptr;     // k_query fused reduce: per-query slab counters (kept zero)
   int qcnt_cap = 0;
-  // $PIR_FUSED_REDUCE=1: k_query's last workgroup XORs the slabs (no k_reduce launch).  Off by
-  // default: measured slower for a lone 2^20 x 1 KiB query (kernel 0.250 vs 0.218 ms; one
-  // workgroup's 256 KiB of cross-XCD sc1 loads outlast a k_reduce launch)
-  bool fused_reduce = false;
+  // k_query's in-kernel reduce (no k_reduce launch), $PIR_FUSED_REDUCE: 0 = off (k_reduce);
+  // 1 = the last workgroup XORs the slabs (measured slower for a lone 2^20 x 1 KiB query: kernel
+  // 0.250 vs 0.218 ms, one workgroup's 256 KiB of cross-XCD sc1 loads outlast a k_reduce
+  // launch); 2 = every workgroup adds its partial to the answer with memory-side atomics
+  // (answers of efs % 4 == 0 bytes at 4-byte aligned addresses; else k_reduce)
+  int fused_reduce = 0;
+  uint32_t red_gen = 0;  // mode 2: this launch's zeroing flag value (never 0)
   uint8_t* d_coef_stage = nullptr;  // explicit-coefficient answers: host vectors staged here
   size_t coef_stage_cap = 0;
   uint8_t* d_mpkey = nullptr;       // multiparty DPF keys: host keys / unaligned device keys
@@ -301,8 +304,17 @@ int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, 
   const pir::ScanShape& sh = qp.shape;
   int rc = ensure_slabs(e, (size_t)nk * pir::query_slab_bytes(qp));
   if (!rc) rc = ensure_buf(&e->d_qscratch, &e->qscratch_cap, pir::query_scratch_bytes(qp));
-  if (!rc && e->fused_reduce) rc = ensure_qcnt(e, nk, s);
+  // mode 2 needs whole answer words at aligned addresses; otherwise k_reduce
+  const int fred = e->fused_reduce == 2 && (c.record_bytes % 4 != 0 ||
+                                            reinterpret_cast<uintptr_t>(d_out) % 4 != 0)
+                       ? 0 : e->fused_reduce;
+  if (!rc && fred) rc = ensure_qcnt(e, nk, s);
   if (rc) return rc;
+  uint32_t gen = 0;
+  if (fred == 2) {
+    if (++e->red_gen == 0) ++e->red_gen;
+    gen = e->red_gen;
+  }
   e->last_chunks = 1;
   e->last_fused = 2;
   hipEvent_t* ev = e->ev;
@@ -316,12 +328,12 @@ int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, 
   HIP_TRY(pir::launch_query(qp, d_raw, (uint32_t)e->key_len, nk, c.num_parties,
                             c.log_num_records, c.party_index - 1, log_parts_total, prefix,
                             e->d_shard + row0 * e->pitch, e->d_slabs, e->d_qscratch, s, nullptr,
-                            e->fused_reduce ? d_out : nullptr, e->d_qcnt, c.record_bytes));
+                            fred ? d_out : nullptr, e->d_qcnt, c.record_bytes, gen));
   if (ev) {
     HIP_TRY(hipEventRecord(ev[EV_SCAN_E], s));
     HIP_TRY(hipEventRecord(ev[EV_PRERED], s));
   }
-  if (!e->fused_reduce) HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, d_out, s, nk));
+  if (!fred) HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, d_out, s, nk));
   if (ev) HIP_TRY(hipEventRecord(ev[EV_RED], s));
   return PIR_OK;
 }
@@ -774,7 +786,7 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
     const char* qy = getenv("PIR_QUERY");
     e->allow_query = !(qy && qy[0] == '0');
     const char* fr = getenv("PIR_FUSED_REDUCE");
-    e->fused_reduce = fr && fr[0] == '1';
+    if (fr) e->fused_reduce = std::max(0, std::min(2, atoi(fr)));
     const char* bg = getenv("PIR_BATCH_G");
     if (bg) e->batch_group = atoi(bg);
     const char* bb = getenv("PIR_BATCH_SCAN_BPC");

@@ -173,12 +173,14 @@ constexpr int kQueryTraceSlots = 192;  // trace: per-workgroup phase stamps (wal
 // device scratch for the super-tile tile inputs (0 when ls == 0)
 size_t query_scratch_bytes(const QueryPlan& qp);
 // out != nullptr: the answers are reduced in-kernel (no launch_reduce): query k's nq x efs bytes
-// at out + k * nq * efs; qcnt = nk zeroed counters (the kernel leaves them zero)
+// at out + k * nq * efs.  gen == 0: qcnt = nk zeroed counters (the kernel leaves them zero),
+// the last workgroup reduces; gen != 0: every workgroup adds its partial with memory-side
+// atomics, qcnt[0] = the launch's zeroing flag (gen unique per launch; efs % 4 == 0)
 hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
                         int p, int n, int party0, int log_parts, uint64_t prefix,
                         const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
                         uint64_t* trace = nullptr, uint8_t* out = nullptr,
-                        uint32_t* qcnt = nullptr, uint32_t efs = 0);
+                        uint32_t* qcnt = nullptr, uint32_t efs = 0, uint32_t gen = 0);
 // XOR the slabs, compact pitch -> record_bytes: d_out[a*efs + b]; nk queries (slabs of query k
 // grid.x*grid.y*slab_bytes apart, answers nq*efs bytes apart)
 hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t efs,

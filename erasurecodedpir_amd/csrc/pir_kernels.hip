@@ -1164,9 +1164,13 @@ __global__ __launch_bounds__(NT) void k_query(
     uint4* __restrict__ fr_s, uint32_t* __restrict__ fr_t, const uint8_t* __restrict__ shard,
     uint32_t pitch, uint32_t cpr, uint32_t gy, uint8_t* __restrict__ slabs,
     uint64_t* __restrict__ trace, uint8_t* __restrict__ out, uint32_t* __restrict__ qcnt,
-    uint32_t efs) {
+    uint32_t efs, uint32_t red_gen) {
   // out != nullptr: the slabs of each query are reduced in-kernel into out (query k at
-  // out + k * nq * efs; qcnt[k] zero on entry, left zero); else the host launches k_reduce.
+  // out + k * nq * efs); else the host launches k_reduce.  red_gen == 0: the last workgroup to add
+  // to qcnt[k] (zero on entry, left zero) XORs every slab.  red_gen != 0 (efs % 4 == 0, out 4-byte
+  // aligned): every workgroup XORs its partial answer into out with memory-side atomics, after
+  // workgroup 0 has zeroed out (stores past L2) and published red_gen in qcnt[0] -- no slab
+  // traffic and no single-workgroup tail.
   // trace != nullptr: per-workgroup wall-clock stamps (100 MHz) of query 0's phases,
   // kQueryTraceSlots apart (layout: pir_engine_trace_query, include/pir_engine.h)
   // diagnostics only: trace[kQueryTraceSlots * gridDim.x] bit 0 = scan waves skip their rows
@@ -1191,7 +1195,19 @@ __global__ __launch_bounds__(NT) void k_query(
     sm.bar = 0; sm.sbar = 0; sm.ready = 0;
     for (int r = 0; r < RING; ++r) sm.consumed[r] = 0;
   }
+  const bool atomic_red = out && red_gen;
+  if (atomic_red && blockIdx.x == 0) {  // zero every queued answer, past this XCD's L2
+    uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
+    const uint32_t words = (uint32_t)nk * NQ * (efs / 4);
+    for (uint32_t i = threadIdx.x; i < words; i += NT)
+      __hip_atomic_store(o32 + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  }
   __syncthreads();
+  if (atomic_red && blockIdx.x == 0 && threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(qcnt, red_gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (trace && threadIdx.x == 0) trace[1] = wall_clock64();
 
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1681,6 +1697,27 @@ __global__ __launch_bounds__(NT) void k_query(
         group_barrier(&sm.sbar, sgen, SW);  // every scan wave's planes are in red[]
         uint32_t* qslab = reinterpret_cast<uint32_t*>(slabs) + qy * slab_q_words;
         const int st = (int)threadIdx.x - TW * 64;
+        if (atomic_red) {
+          // the workgroup's partial answer straight into out (memory-side atomics), once
+          // workgroup 0's zeros are published (long done by now: a wait that never spins)
+          if (st == 0)
+            while (__hip_atomic_load(qcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != red_gen)
+              __builtin_amdgcn_s_sleep(2);
+          group_barrier(&sm.sbar, sgen, SW);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          uint32_t* o32 = reinterpret_cast<uint32_t*>(out + (size_t)qy * NQ * efs);
+          const uint32_t wpr = efs / 4;  // answer words per round
+          for (uint32_t gg = 0; gg < gy; ++gg)
+            for (int k = st; k < (int)slab_words; k += SW * 64) {
+              const uint32_t a = (uint32_t)k / GW, w = gg * GW + (uint32_t)k % GW;
+              const uint32_t v = sm.red[gg][k];
+              sm.red[gg][k] = 0;
+              if (v && w < wpr) atomicXor(o32 + a * wpr + w, v);
+            }
+          group_barrier(&sm.sbar, sgen, SW);  // red[] is clear for the next query
+          if (trace && qy == 0 && sw == 0 && lane == 0) trace[6] = wall_clock64();
+          continue;
+        }
         for (uint32_t gg = 0; gg < gy; ++gg) {
           uint32_t* slab = qslab + ((uint64_t)gg * gridDim.x + blockIdx.x) * slab_words;
           for (int k = st; k < (int)slab_words; k += SW * 64) {
@@ -2109,7 +2146,8 @@ template <int NQ, int TILE>
 static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
                            int p, int n, int party0, int log_parts, uint64_t prefix,
                            const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
-                           uint64_t* trace, uint8_t* out, uint32_t* qcnt, uint32_t efs) {
+                           uint64_t* trace, uint8_t* out, uint32_t* qcnt, uint32_t efs,
+                           uint32_t gen) {
   uint4* fr_s = reinterpret_cast<uint4*>(scratch);
   uint32_t* fr_t = reinterpret_cast<uint32_t*>(scratch + ((size_t)qp.shape.grid.x << (kQueryKin + qp.ls)) * sizeof(uint4));
   constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : 8));
@@ -2120,7 +2158,7 @@ static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t k
   hipLaunchKernelGGL((k_query<NQ, NRP, VEC, UNI, TW, TILE, GY, RING, NTH>), dim3(sh.grid.x),     \
                      dim3(NTH), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,                    \
                      log_parts, prefix, qp.lr, qp.lt, qp.ls, fr_s, fr_t, shard, sh.pitch, sh.cpr,  \
-                     gy, slabs, trace, out, qcnt, efs)
+                     gy, slabs, trace, out, qcnt, efs, gen)
 #define PIR_QL(UNI, TW, GY, gy) PIR_QLN(UNI, TW, GY, gy, kFusedThreads)
   if constexpr (VEC == 2 && NQ >= 4 && NQ <= 5 && NQ > PIR_QUERY_BRANCH_MAXNQ && TILE == 1024) {
     if (sh.uniform && qp.m4r) {  // four-Russians scan waves (k_query's kM4R)
@@ -2150,9 +2188,12 @@ size_t query_scratch_bytes(const QueryPlan& qp) {
 hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
                         int p, int n, int party0, int log_parts, uint64_t prefix,
                         const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
-                        uint64_t* trace, uint8_t* out, uint32_t* qcnt, uint32_t efs) {
+                        uint64_t* trace, uint8_t* out, uint32_t* qcnt, uint32_t efs,
+                        uint32_t gen) {
   if (nk < 1 || (qp.ls && !scratch) || (out && !qcnt)) return hipErrorInvalidValue;
-#define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, scratch, s, trace, out, qcnt, efs)
+  if (out && gen && (efs % 4 != 0 || reinterpret_cast<uintptr_t>(out) % 4 != 0))
+    return hipErrorInvalidValue;
+#define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, scratch, s, trace, out, qcnt, efs, gen)
 #ifdef PIR_DEV_NQ  // development builds only (ISA / register checks): one round count
   return qp.shape.nq == PIR_DEV_NQ && qp.tile == 1024 ? PIR_Q(PIR_DEV_NQ, 1024) : hipErrorInvalidValue;
 #else
