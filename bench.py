@@ -320,6 +320,9 @@ def measure(ctx, eng, keys, W, K, single=True):
     the same K queries one launch each.  keys: party-1 keys (W + K of them)."""
     kl, ab = eng.key_len, eng.answer_bytes
     nkeys = W + K
+    if len(keys) < nkeys:
+        raise ValueError(f"measure: {len(keys)} keys for a warm-up of {W} and {K} timed queries")
+    keys = keys[:nkeys]  # callers may pass more (the 1-GPU reference reuses the N-GPU key set)
     d_keys = eng.alloc_dev(kl * nkeys)
     d_res = eng.alloc_dev(ab * nkeys)
     eng.h2d(d_keys, b"".join(keys))
@@ -606,7 +609,8 @@ def main():
             e1 = pir.Engine(p, 1, n, efs, nq, device=local)
             e1.fill_shard_random(SHARD_SEED)
             solo = Ctx(1, 0, local)
-            m1 = measure(solo, e1, [ks[0] for _, ks in keyset], min(W, 2), K, single=False)
+            W1 = min(W, 2)  # the same K timed queries as the split-shard run (keys W .. W+K-1)
+            m1 = measure(solo, e1, [ks[0] for _, ks in keyset][W - W1:], W1, K, single=False)
             e1.close()
             v1 = shard_bytes / GIB / (m1["ms"] / 1e3)
             out["n1_reference"] = {
