@@ -74,6 +74,7 @@ PROTOTYPES = {
     "pir_engine_set_shard_rows": (_I, [_P, _P, _U64, _U64]),
     "pir_engine_fill_shard_random": (_I, [_P, _U64]),
     "pir_engine_encode_across_dev": (_I, [_P, _P, _U64, _U64, _I]),
+    "pir_engine_encode_within_dev": (_I, [_P, _P, _U64, _U64, ctypes.c_uint32, _I, _I]),
     "pir_engine_get_shard_row": (_I, [_P, _U64, _P]),
     "pir_engine_get_shard": (_I, [_P, _U64, _U64, _P]),
     "pir_engine_answer": (_I, [_P, _P, _P]),

@@ -917,6 +917,29 @@ int pir_engine_encode_across_dev(pir_engine_t* e, const uint8_t* d_files, uint64
   return PIR_OK;
 }
 
+int pir_engine_encode_within_dev(pir_engine_t* e, const uint8_t* d_files, uint64_t file_pitch,
+                                 uint64_t num_files, uint32_t file_bytes, int k, int party) {
+  if (!e) return fail(PIR_EINVAL, "null engine");
+  if (k < 1 || k > 16) return fail(PIR_EINVAL, "k = %d outside [1,16]", k);
+  if (party < 0 || party > 255) return fail(PIR_EINVAL, "party %d outside [0,255]", party);
+  if (d_files && file_pitch < file_bytes) return fail(PIR_EINVAL, "file_pitch < file_bytes");
+  if ((uint64_t)file_bytes > (uint64_t)k * e->cfg.record_bytes)
+    return fail(PIR_EINVAL, "file_bytes %u > k * record_bytes (%d * %u)", file_bytes, k,
+                e->cfg.record_bytes);
+  if (num_files > (1ull << e->cfg.log_num_records))
+    return fail(PIR_EINVAL, "%llu files > 2^%d rows", (unsigned long long)num_files,
+                e->cfg.log_num_records);
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const uint64_t row0 = (uint64_t)e->cfg.partition_index * e->rows;
+  HIP_TRY(pir::launch_encode_within(d_files, file_pitch, num_files, file_bytes, k,
+                                    party ? party : e->cfg.party_index, e->d_shard, e->rows,
+                                    row0, e->pitch,
+                                    e->cfg.record_bytes, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return PIR_OK;
+}
+
 int pir_engine_get_shard_row(pir_engine_t* e, uint64_t row, uint8_t* out) {
   if (!e || !out) return fail(PIR_EINVAL, "null argument");
   if (row >= e->rows) return fail(PIR_EINVAL, "row %llu beyond shard", (unsigned long long)row);

@@ -291,16 +291,11 @@ std::string setup(const MVal& req) {  // server.go:295-331
     if (pir_engine_encode_across_dev(g.eng, nullptr, 0, (uint64_t)NUM_FILES, K) != PIR_OK)
       return std::string("encode: ") + pir_engine_last_error();
   } else {
-    // encoded within files (client.cpp:99-103) on the host by the shim, then uploaded
-    client cl{};
-    server sv{};
-    initialize_client(&cl, (uint8_t)LOG_NUM_FILES, FILE_SIZE_BYTES);
-    initializeServer(&sv, g.party, LOG_NUM_FILES, (uint32_t)ENCODED_FILE_SIZE_BYTES, 0, 1);
-    encode_within_files_server(&cl, &sv);
-    const int rc = pir_engine_set_shard_rows(g.eng, sv.indexList, 0, (uint64_t)NUM_ENCODED_FILES);
-    freeServer(&sv);
-    free_client(&cl);
-    if (rc != PIR_OK) return std::string("upload: ") + pir_engine_last_error();
+    // the synthetic database of client.cpp:16-33, encoded within files (client.cpp:99-103) on
+    // the GPU: no host copy of the database, no host encode under the lock
+    if (pir_engine_encode_within_dev(g.eng, nullptr, 0, (uint64_t)NUM_FILES, FILE_SIZE_BYTES, K,
+                                     g.party) != PIR_OK)
+      return std::string("encode: ") + pir_engine_last_error();
   }
   g.mode = mode;
   g.nq = rounds;

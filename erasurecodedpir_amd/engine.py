@@ -96,6 +96,25 @@ class Engine:
             if d_f is not None:
                 self.free_dev(d_f)
 
+    def encode_within(self, num_files, file_bytes, k, files=None, party=0):
+        """The Hollanti-mode shard (encoded within files) computed on the GPU (client.cpp:43-56,
+        99-103): from `files` (num_files x file_bytes host array) or, files=None, the
+        reference's synthetic database (client.cpp:16-33).  party: the server's party index
+        (0: the engine's)."""
+        d_f, pitch = None, 0
+        if files is not None:
+            f = np.ascontiguousarray(np.asarray(files, np.uint8).reshape(num_files, -1))
+            pitch = f.shape[1]
+            d_f = self.alloc_dev(f.size)
+        try:
+            if d_f is not None:
+                self.h2d(d_f, f.reshape(-1))
+            check(self._lib.pir_engine_encode_within_dev(self._h, d_f, pitch, num_files,
+                                                         file_bytes, k, party), "encode_within")
+        finally:
+            if d_f is not None:
+                self.free_dev(d_f)
+
     def shard_row(self, i):
         out = np.empty(self.record_bytes, np.uint8)
         check(self._lib.pir_engine_get_shard_row(self._h, i, out.ctypes.data_as(ctypes.c_void_p)),

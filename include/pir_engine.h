@@ -86,6 +86,16 @@ int pir_engine_fill_shard_random(pir_engine_t *e, uint64_t seed);
  * reference's synthetic database (client.cpp:16-33). */
 int pir_engine_encode_across_dev(pir_engine_t *e, const uint8_t *d_files, uint64_t file_pitch,
                                  uint64_t num_files, int k);
+/* the Hollanti-mode shard (MODE 3: encoded within files), computed on the GPU (client.cpp:43-56,
+ * 99-103; replaces the host encode_within_files_server of the server setup): row r of this
+ * engine's rows = XOR_{j<k} gf_pow(party, j) * part j of file r, part j = bytes
+ * [j*record_bytes, (j+1)*record_bytes) of the file, zero past file_bytes; rows >= num_files are
+ * zero.  d_files: num_files device rows file_pitch >= file_bytes bytes apart, or NULL for the
+ * reference's synthetic database (client.cpp:16-33).  party: the server's party index (1..),
+ * or 0 for the engine's party_index (a Hollanti engine is created with 2 parties: they only
+ * size tree-DPF keys). */
+int pir_engine_encode_within_dev(pir_engine_t *e, const uint8_t *d_files, uint64_t file_pitch,
+                                 uint64_t num_files, uint32_t file_bytes, int k, int party);
 int pir_engine_get_shard_row(pir_engine_t *e, uint64_t row, uint8_t *out);
 /* rows [row0, row0+nrows) back to the host, record_bytes per row, packed */
 int pir_engine_get_shard(pir_engine_t *e, uint64_t row0, uint64_t nrows, uint8_t *out);

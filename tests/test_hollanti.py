@@ -166,3 +166,46 @@ def test_gpu_answer_coefs_full_size_linearity():
     assert np.array_equal(delta[a], tab[rec])
     assert not delta[[r for r in range(nq) if r != a]].any()
     assert np.array_equal(dev, base)
+
+
+# ---------------------------------------------------------- the Hollanti shard on the GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("ci", range(4))
+def test_gpu_encode_within_matches_reference(ci):
+    """k_encode_within (pir_engine_encode_within_dev: the server setup of MODE 3 in pir_serve)
+    == the reference's encode_within_files_server rows (per-party shard hash), from the
+    synthetic database and from explicit files."""
+    import erasurecodedpir_amd as pir
+    case = O.golden("hollanti.json")["cases"][ci]
+    L, f, efs, k, nq = case["L"], case["f"], case["efs"], case["k"], case["nq"]
+    files = O.synthetic_db(L, f).reshape(1 << L, f)
+    for party in range(case["p"]):
+        with pir.Engine(2, 1, L, efs, nq) as e:
+            e.encode_within(1 << L, f, k, party=party + 1)
+            assert O.sha(e.get_shard()) == case["shard_sha256"][party], party
+            e.encode_within(1 << L, f, k, files=files, party=party + 1)
+            assert O.sha(e.get_shard()) == case["shard_sha256"][party], party
+
+
+@pytest.mark.gpu
+def test_gpu_encode_within_random_files_and_partitions():
+    """Random files, a file size that is not a multiple of k, split-shard partitions: the GPU
+    rows equal a numpy restatement of client.cpp:99-103 (coefficients gf_pow(party, j))."""
+    import erasurecodedpir_amd as pir
+    L, f, k, party = 12, 1000, 3, 4
+    efs = -(-f // k)
+    rng = np.random.default_rng(9)
+    files = rng.integers(0, 256, (1 << L, f), dtype=np.uint8)
+    pad = np.zeros((1 << L, k * efs), np.uint8)
+    pad[:, :f] = files
+    want = np.zeros((1 << L, efs), np.uint8)
+    for j in range(k):
+        c = O.gf_pow(party, j)
+        tab = np.array([O.gf_mul(x, c) for x in range(256)], np.uint8)
+        want ^= tab[pad[:, j * efs:(j + 1) * efs]]
+    G = 2
+    rows = (1 << L) >> G
+    for part in range(1 << G):
+        with pir.Engine(2, 1, L, efs, 1, log_num_partitions=G, partition_index=part) as e:
+            e.encode_within(1 << L, f, k, files=files, party=party)
+            assert np.array_equal(e.get_shard(), want[part * rows:(part + 1) * rows]), part
