@@ -114,15 +114,28 @@ __device__ __forceinline__ uint32_t last_col(const Tab& T, uint32_t a, uint32_t 
   return x ^ k;
 }
 
+// the first NB (1-3) bytes of a last-round column, AddRoundKey included (the others: don't care)
+template <int NB>
+__device__ __forceinline__ uint32_t last_col_b(const Tab& T, uint32_t a, uint32_t b, uint32_t c,
+                                               uint32_t k) {
+  uint32_t x = T.t2<0>(a);  // byte 0 = S[a.b0]
+  if constexpr (NB >= 2) x = (x & 0xffu) | (T.t0<1>(b) & 0xff00u);
+  if constexpr (NB >= 3) x |= T.t0<2>(c) & 0xff0000u;
+  return x ^ k;
+}
+
 constexpr uint32_t kRcon[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
 
 // Row shape, one key, NB CTR blocks with counters c0..c0+NB-1 (c0 a multiple of NB, NB <= 256,
 // passed as ctr_be = the byte-swapped c0, i.e. BE128(c0)'s last word); block NB-1 only needs its
 // first LASTW output words (the control-bit bytes); out[b] = AES_key(BE128(c0 + b)).  The
-// counters differ in byte 15 only.
-template <int NB, int LASTW>
+// counters differ in byte 15 only.  LASTB in 1-3 (one block): only the first LASTB output
+// bytes are valid (a leaf's 1-2 share bytes): LASTB last-round lookups, the last key word's
+// bytes alone, and the ninth round's columns nothing reads are dropped by the compiler.
+template <int NB, int LASTW, int LASTB = 0>
 __device__ __forceinline__ void aes_ctr_row(const Tab& T, uint4 key, uint4 (&out)[NB],
                                             uint32_t ctr_be = 0) {
+  static_assert(LASTB == 0 || (NB == 1 && LASTB < 4), "byte-trimmed: one block, 1-3 bytes");
   uint32_t k0 = key.x, k1 = key.y, k2 = key.z, k3 = key.w;
   uint32_t w[NB][4];
 #pragma unroll
@@ -169,6 +182,14 @@ __device__ __forceinline__ void aes_ctr_row(const Tab& T, uint4 key, uint4 (&out
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) round_row(T, w[b][0], w[b][1], w[b][2], w[b][3], r0, r1, r2, r3);
+  }
+  if constexpr (LASTB > 0) {
+    // k0 of the last round key, bytes < LASTB: k0 ^ SubWord(RotWord(k3)) ^ rcon
+    uint32_t t = T.t2<1>(k3);  // byte 0 = S[k3.b1]
+    if constexpr (LASTB >= 2) t = (t & 0xffu) | (T.t0<2>(k3) & 0xff00u);
+    if constexpr (LASTB >= 3) t |= T.t0<3>(k3) & 0xff0000u;
+    out[0] = make_uint4(last_col_b<LASTB>(T, w[0][0], w[0][1], w[0][2], k0 ^ t ^ kRcon[9]), 0, 0, 0);
+    return;
   }
   key_next(T, k0, k1, k2, k3, kRcon[9]);
   const uint32_t kk[4] = {k0, k1, k2, k3};

@@ -281,7 +281,7 @@ __global__ __launch_bounds__(kExpThreads) void k_expand(
   if (k == 0) {  // FINAL only: the input nodes are the leaves
     __syncthreads();
     for (int i = threadIdx.x; i < tile; i += blockDim.x) {
-      const uint4 v = leaf_value<NW>(T, K, B.pm1, in_s[ibase + i], in_t[ibase + i]);
+      const uint4 v = leaf_value<NW, (NRP < 4 ? NRP : 0)>(T, K, B.pm1, in_s[ibase + i], in_t[ibase + i]);
       store_leaf<NRP>(c, obase + i, make_uint4(v.x & qm.x, v.y & qm.y, v.z & qm.z, v.w & qm.w), cstride);
     }
     return;
@@ -322,8 +322,8 @@ __global__ __launch_bounds__(kExpThreads) void k_expand(
     uint32_t tl, tr;
     expand_node(T, K, L, B, is[u], it[u], sl, sr, tl, tr);
     if constexpr (FINAL) {
-      const uint4 vl = leaf_value<NW>(T, K, B.pm1, sl, tl);
-      const uint4 vr = leaf_value<NW>(T, K, B.pm1, sr, tr);
+      const uint4 vl = leaf_value<NW, (NRP < 4 ? NRP : 0)>(T, K, B.pm1, sl, tl);
+      const uint4 vr = leaf_value<NW, (NRP < 4 ? NRP : 0)>(T, K, B.pm1, sr, tr);
       if (NRP == 1 && cstride == 1) {  // both leaves in one 16-bit store
         *reinterpret_cast<uint16_t*>(c + obase + 2 * u) =
             (uint16_t)((vl.x & qm.x & 0xffu) | ((vr.x & qm.x & 0xffu) << 8));
@@ -963,8 +963,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
           uint4 sl, sr;
           uint32_t tl, tr;
           expand_node(T, K, L, B, is[u], it[u], sl, sr, tl, tr);
-          uint4 vl = leaf_value<NW>(T, K, B.pm1, sl, tl);
-          uint4 vr = leaf_value<NW>(T, K, B.pm1, sr, tr);
+          uint4 vl = leaf_value<NW, (NRP < 4 ? NRP : 0)>(T, K, B.pm1, sl, tl);
+          uint4 vr = leaf_value<NW, (NRP < 4 ? NRP : 0)>(T, K, B.pm1, sr, tr);
           vl = make_uint4(vl.x & qm.x, vl.y & qm.y, vl.z & qm.z, vl.w & qm.w);
           vr = make_uint4(vr.x & qm.x, vr.y & qm.y, vr.z & qm.z, vr.w & qm.w);
           if constexpr (NRP == 1) {
@@ -1459,8 +1459,8 @@ __global__ __launch_bounds__(NT) void k_query(
           const uint32_t tb = (o[2].x & B.tb_mask) ^ ct;
           const uint32_t tl = tb & B.tmask, tr = (tb >> B.pm1) & B.tmask;
           uint4 vl[1], vr[1];
-          aes_ctr_row<1, NW>(T, xor4(o[0], cs), vl);
-          aes_ctr_row<1, NW>(T, xor4(o[1], cs), vr);
+          aes_ctr_row<1, NW, (NRP < 4 ? NRP : 0)>(T, xor4(o[0], cs), vl);
+          aes_ctr_row<1, NW, (NRP < 4 ? NRP : 0)>(T, xor4(o[1], cs), vr);
           for (uint32_t j = 0; j < pm1; ++j) {
             vl[0] = xor4(vl[0], and4(sm.lastcw[j], 0u - ((tl >> j) & 1u)));
             vr[0] = xor4(vr[0], and4(sm.lastcw[j], 0u - ((tr >> j) & 1u)));

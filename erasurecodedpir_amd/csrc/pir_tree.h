@@ -61,12 +61,12 @@ __device__ __forceinline__ void store_leaf(uint8_t* __restrict__ c, uint64_t lea
   else *reinterpret_cast<uint4*>(dst) = v;
 }
 
-// leaf value (before masking to nq bytes)
-template <int NW>
+// leaf value (before masking to nq bytes); LASTB 1-3: only that many bytes valid
+template <int NW, int LASTB = 0>
 __device__ __forceinline__ uint4 leaf_value(const Tab& T, const DevKey* __restrict__ K,
                                             uint32_t pm1, uint4 seed, uint32_t t) {
   uint4 o[1];
-  aes_ctr_row<1, NW>(T, seed, o);
+  aes_ctr_row<1, NW, LASTB>(T, seed, o);
   for (uint32_t j = 0; j < pm1; ++j) o[0] = xor4(o[0], and4(K->lastcw[j], 0u - ((t >> j) & 1u)));
   return o[0];
 }
