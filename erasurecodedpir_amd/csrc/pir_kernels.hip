@@ -405,6 +405,30 @@ __device__ __forceinline__ uint32_t m4r_index(uint64_t w0, uint64_t w1, uint64_t
       : "s"(w0), "s"(w1), "s"(w2), "s"(w3));
   return vi;
 }
+// m4r_fold4p's packed indices: lane 8a + 7 <- the OR of lanes 8a .. 8a + 7's indices, each
+// shifted to bits [4b, 4b + 4) (sh = 4 (lane % 8)) -- three row_shr DPP ORs, so a group takes NA
+// v_readlane of its indices instead of 8 NA ($PIR_M4R_PACKED=0 at build time: the unpacked fold)
+#ifndef PIR_M4R_PACKED
+#define PIR_M4R_PACKED 1
+#endif
+__device__ __forceinline__ uint32_t m4r_pack(uint32_t vi, uint32_t sh) {
+  uint32_t t = vi << sh;
+  t |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x111, 0xf, 0xf, true);  // row_shr:1
+  t |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x112, 0xf, 0xf, true);  // row_shr:2
+  t |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x114, 0xf, 0xf, true);  // row_shr:4
+  return t;
+}
+template <int VEC, int NA>
+__device__ __forceinline__ void m4r_fold_group(uint32_t (&Z)[NA][8][VEC], const uint32_t* x0,
+                                               const uint32_t* x1, const uint32_t* x2,
+                                               const uint32_t* x3, uint32_t vi, uint32_t sh) {
+#if PIR_M4R_PACKED
+  m4r_fold4p<VEC, NA>(Z, x0, x1, x2, x3, m4r_pack(vi, sh));
+#else
+  (void)sh;
+  m4r_fold4<VEC, NA>(Z, x0, x1, x2, x3, vi);
+#endif
+}
 // row j's coefficient word from the lanes holding a 64-row block's coefficients (x: rounds 0-3,
 // y: rounds 4-7)
 __device__ __forceinline__ uint64_t coef_word(const uint4& c4, uint32_t j) {
@@ -746,7 +770,7 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
         for (uint32_t j0 = 0; j0 < nb; j0 += 4) {
           const uint32_t vi = m4r_index(coef_word(c4, j0), coef_word(c4, j0 + 1),
                                         coef_word(c4, j0 + 2), coef_word(c4, j0 + 3));
-          m4r_fold4<VEC, NQ>(Z, x[0].v, x[1].v, x[2].v, x[3].v, vi);
+          m4r_fold_group<VEC, NQ>(Z, x[0].v, x[1].v, x[2].v, x[3].v, vi, (lane & 7u) * 4u);
 #pragma unroll
           for (int r = 0; r < 4; ++r) load_row(rb + j0 + r + U, x[r]);
           __builtin_amdgcn_sched_barrier(0);
@@ -1633,7 +1657,8 @@ __global__ __launch_bounds__(NT) void k_query(
             for (int g4 = 0; g4 < U; g4 += 4) {
               const uint32_t vi = m4r_index(coef_word(c4, g4), coef_word(c4, g4 + 1),
                                             coef_word(c4, g4 + 2), coef_word(c4, g4 + 3));
-              m4r_fold4<VEC, NQ>(Z, x[g4].v, x[g4 + 1].v, x[g4 + 2].v, x[g4 + 3].v, vi);
+              m4r_fold_group<VEC, NQ>(Z, x[g4].v, x[g4 + 1].v, x[g4 + 2].v, x[g4 + 3].v, vi,
+                                      (lane & 7u) * 4u);
 #pragma unroll
               for (int r = 0; r < 4; ++r) load_slot(gn, jn + g4 + r, x[g4 + r]);
               __builtin_amdgcn_sched_barrier(0);

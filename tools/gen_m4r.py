@@ -84,6 +84,74 @@ __device__ __forceinline__ void m4r_fold4<{vec}, {na}>(uint32_t (&Z)[{na}][8][{v
 """
 
 
+def fold_packed(vec, na):
+    """The same fold with the plane indices packed 8 to a dword (lane 8a + 7 of vp holds round a's:
+    bits [4b, 4b + 4) = plane (a, b)'s index): NA v_readlane per group instead of 8 NA, each index
+    extracted by s_bfe_u32 -- placed between s_set_gpr_idx_idx and the plane's v_xor, so it is
+    that index change's wait state too (no s_nop)."""
+    base = 128 - 16 * vec
+    # vp comes straight from m4r_pack's last DPP v_or: a v_readlane of it right behind that
+    # write read the value before it (round 0's indices of planes 0-3 lost, the readlanes one
+    # instruction later right: 4-round 768-thread k_scan_uni, tools/diag/m4r_rounds.py) -- the
+    # compiler's hazard recognizer does not see into this statement, so wait here
+    lines = ["s_nop 4"]
+    lines += [f"v_readlane_b32 %[p{a}], %[vp], {8 * a + 7}" for a in range(na)]
+    lines.append("s_mov_b32 %[m0s], m0")
+    n = 8 * na
+    # an index change reads an SGPR the SALU wrote: keep every extract >= 6 instructions before
+    # its s_set_gpr_idx_* (3 planes ahead, 4 SGPRs in rotation; the first 3 sit amid the
+    # combinations, >= 8 instructions after the readlanes and before the window opens)
+    ahead = 3
+    def reg(k):
+        return f"s{k % (ahead + 1)}"
+    def bfe(k):
+        return f"s_bfe_u32 %[{reg(k)}], %[p{k // 8}], {hex((4 << 16) | (4 * (k % 8)))}"
+    comb = []
+    for v in range(vec):
+        comb += combos(base + 16 * v, [f"%[x{i}{v}]" for i in range(4)])
+    lines += comb[:8] + [bfe(k) for k in range(min(ahead, n))] + comb[8:]
+    lines.append("s_set_gpr_idx_on %[s0], gpr_idx(SRC0)")
+    for k in range(n):
+        if k + ahead < n:
+            lines.append(bfe(k + ahead))
+        lines.append("@PACK_WAIT" if k + ahead < n else "@NOP_IDX")
+        a, b = divmod(k, 8)
+        for v in range(vec):
+            z = (a * vec + v) * 8 + b
+            lines.append(f"v_xor_b32 %{z}, v{base + 16 * v}, %{z}")
+        if k + 1 < n:
+            lines.append(f"s_set_gpr_idx_idx %[{reg(k + 1)}]")
+    lines.append("s_set_gpr_idx_off")
+    lines.append("s_mov_b32 m0, %[m0s]")
+    def emit(ln):
+        if ln == "@NOP_IDX":
+            return "      PIR_M4R_NOP_IDX"
+        if ln == "@PACK_WAIT":
+            return "      PIR_M4R_PACK_NOP"
+        return f'      "{ln}\\n\\t"'
+    body = "\n".join(emit(ln) for ln in lines)
+    zops = ", ".join(f'"+v"(Z[{a}][{b}][{v}])' for a in range(na) for v in range(vec)
+                     for b in range(8))
+    sops = ", ".join([f'[p{a}] "=&s"(p{a})' for a in range(na)] +
+                     [f'[s{i}] "=&s"(s{i})' for i in range(ahead + 1)] + ['[m0s] "=&s"(m0s)'])
+    xins = ", ".join(f'[x{i}{v}] "v"(x{i}[{v}])' for i in range(4) for v in range(vec))
+    clob = ", ".join([f'"v{r}"' for r in range(base, 128)] + ['"scc"'])
+    pdecl = ", ".join(f"p{a}" for a in range(na))
+    return f"""template <>
+__device__ __forceinline__ void m4r_fold4p<{vec}, {na}>(uint32_t (&Z)[{na}][8][{vec}], const uint32_t* x0,
+                                            const uint32_t* x1, const uint32_t* x2,
+                                            const uint32_t* x3, uint32_t vp) {{
+  uint32_t {pdecl}, {", ".join(f"s{i}" for i in range(ahead + 1))}, m0s;
+  asm volatile(
+{body}
+      : {zops},
+        {sops}
+      : {xins}, [vp] "v"(vp)
+      : {clob});
+}}
+"""
+
+
 def main():
     out = ['// GENERATED by tools/gen_m4r.py -- do not edit.  Four-Russians plane folds (see there).',
            '#pragma once', '#include <hip/hip_runtime.h>', '#include <stdint.h>', '',
@@ -98,16 +166,26 @@ def main():
            '// last partial group re-read row r0 with the next wave\'s coefficients (708a01d: 3 x 2^20',
            '// rows, 2048 per wave, every variant right).  The engine\'s scans fold whole 4-row groups',
            '// whose rows past the end have zero coefficients.',
-           '#ifndef PIR_M4R_NOP_IDX', '#define PIR_M4R_NOP_IDX "s_nop 0\\n\\t"', '#endif', '',
+           '#ifndef PIR_M4R_NOP_IDX', '#define PIR_M4R_NOP_IDX "s_nop 0\\n\\t"', '#endif',
+           '// m4r_fold4p: wait state after each index change besides the next extract',
+           '#if PIR_M4R_PACK_WAIT', '#define PIR_M4R_PACK_NOP "s_nop 0\\n\\t"', '#else',
+           '#define PIR_M4R_PACK_NOP ""', '#endif', '',
            'namespace pir {', '',
            '// Fold 4 rows (x0..x3: VEC dwords each) into NA rounds x 8 bit planes; vi = the plane',
            '// indices, lane 8a + b = bits b of the 4 rows\' round-a coefficients (row i -> bit i).',
            'template <int VEC, int NA>',
            '__device__ __forceinline__ void m4r_fold4(uint32_t (&Z)[NA][8][VEC], const uint32_t* x0,',
            '                                          const uint32_t* x1, const uint32_t* x2,',
-           '                                          const uint32_t* x3, uint32_t vi);', '']
+           '                                          const uint32_t* x3, uint32_t vi);', '',
+           '// The same fold from packed indices: lane 8a + 7 of vp = round a\'s 8 plane indices,',
+           '// plane (a, b) in bits [4b, 4b + 4) (m4r_pack of the per-lane indices).',
+           'template <int VEC, int NA>',
+           '__device__ __forceinline__ void m4r_fold4p(uint32_t (&Z)[NA][8][VEC], const uint32_t* x0,',
+           '                                           const uint32_t* x1, const uint32_t* x2,',
+           '                                           const uint32_t* x3, uint32_t vp);', '']
     for vec, na in VARIANTS:
         out.append(fold(vec, na))
+        out.append(fold_packed(vec, na))
     out.append('}  // namespace pir')
     print("\n".join(out))
 
