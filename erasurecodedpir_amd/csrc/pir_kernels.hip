@@ -20,6 +20,7 @@
 #include "pir_m4r.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <stdlib.h>
 
 namespace pir {
@@ -429,6 +430,16 @@ __device__ __forceinline__ void m4r_fold_group(uint32_t (&Z)[NA][8][VEC], const 
   m4r_fold4<VEC, NA>(Z, x0, x1, x2, x3, vi);
 #endif
 }
+// k_scan_uni's four-Russians groups read their rows' coefficient words by scalar loads
+// ($PIR_M4R_SLOAD=0 at build time: lane loads + v_readlane, as k_query does from its LDS ring)
+#ifndef PIR_M4R_SLOAD
+#define PIR_M4R_SLOAD 1
+#endif
+// a value the wave holds in every lane, as a wave-uniform (SGPR) value
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+}
 // row j's coefficient word from the lanes holding a 64-row block's coefficients (x: rounds 0-3,
 // y: rounds 4-7)
 __device__ __forceinline__ uint64_t coef_word(const uint4& c4, uint32_t j) {
@@ -760,6 +771,40 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
     Chunk<VEC> x[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) load_row(r0 + u, x[u]);
+#if PIR_M4R_SLOAD
+    if constexpr (kM4R) {
+      // the 4 rows' coefficient words straight into SGPRs: scalar loads of the wave-uniform rows
+      // (constant address space), issued one group ahead, after the group's indices are built --
+      // an s_waitcnt lgkmcnt(0) before m4r_index then waits only for loads a whole fold old.
+      // Rows past the wave's last read its last row's word and take 0.
+      using CW = std::conditional_t<NRP == 8, uint64_t, uint32_t>;
+      typedef const __attribute__((address_space(4))) CW* ConstCW;
+      const ConstCW cw = (ConstCW)(const CW*)c;
+      // 32-bit row offsets in the wave's range: SALU compares (no 64-bit s_cmp_lt on gfx950),
+      // and the zeroing select at use, a group after the load
+      const uint64_t u0 = rfl64(r0);
+      const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r1 - r0));
+      const ConstCW cwb = cw + u0;
+      auto raw = [&](uint32_t i) __attribute__((always_inline)) -> uint64_t {
+        return (uint64_t)cwb[i < n ? i : n - 1];
+      };
+      uint64_t w[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = raw(r);
+      for (uint32_t i = 0; i < n; i += 4) {
+        const uint32_t vi = m4r_index(w[0], i + 1 < n ? w[1] : 0, i + 2 < n ? w[2] : 0,
+                                      i + 3 < n ? w[3] : 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[r] = raw(i + 4 + r);
+        m4r_fold_group<VEC, NQ>(Z, x[0].v, x[1].v, x[2].v, x[3].v, vi, (lane & 7u) * 4u);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) load_row(r0 + i + r + U, x[r]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else
+#endif
+    {
     uint4 c4 = coefs64(r0);
     for (uint64_t rb = r0; rb < r1; rb += 64) {
       const uint4 c4n = coefs64(rb + 64);  // the next 64 rows' coefficients, in flight
@@ -828,6 +873,7 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
         }
       }
       c4 = c4n;
+    }
     }
   }
   __syncthreads();  // red[] zeroed
