@@ -596,10 +596,18 @@ def main():
         dist.all_gather_object(allr, mine)
         out["per_rank"] = allr
     cpu_path = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    threads_leg = rank == 0 and world == 1 and not args.no_extras and config == "c24"
+    if rank == 0 and world == 1 and (not args.no_cpu or threads_leg):
         cpu_path = shard_file_path(int(local_bytes))
         dump_shard(eng, cpu_path)
     cpu_key, cpu_want = k0, m["singles"][0]
+    if threads_leg:
+        try:
+            out["threads_c24"] = thread_leg(ctx, pir, eng, [ks[0] for _, ks in timed],
+                                            list(m["singles"]), cpu_path, n, efs)
+        except Exception:
+            os.unlink(cpu_path)
+            raise
     eng.close()
 
     if strong and world > 1:
@@ -635,7 +643,9 @@ def main():
                                                  "ms_per_step", "ms_per_key", "keys_per_s",
                                                  "shard_passes_per_step", "parity")}
         out["configs2_c3b"]["workload"] = b["config"]["workload"]
-    if cpu_path:
+    if cpu_path and args.no_cpu:
+        os.unlink(cpu_path)
+    elif cpu_path:
         try:
             cores = _host_cores() if args.cpu_cores < 0 else args.cpu_cores
             out["cpu_baseline"] = cpu_baseline(cpu_path, n, efs, p, nq, cpu_key, cpu_want,
@@ -706,6 +716,90 @@ def extra_leg(ctx, pir, config, W, K, rng, single=True):
                                "note": "batch = 1: one launch per query"}
         res["queue_equals_one_at_a_time"] = bool(np.array_equal(m["answers"], m["singles"]))
     return res
+
+
+def thread_leg(ctx, pir, eng, keys, want, shard_path, n, efs, T=16, K=10):
+    """The reference's own call shape for a query (src/server_util/tree.go:60-76): T goroutines
+    each call runOptimizedDPFTreeQueryThread(s, key, t, T) on ONE server (T = 16: the AWS
+    config's threads, bench/run_tests.py:180), then assemblDPFTreeQueryThreadResults -- here T
+    persistent Python threads through the pir_server.h shim (ctypes drops the GIL), released
+    together per query.  The shim answers every slice of a query from one engine pass
+    (pir_engine_answer_slices).  Host-API times (key upload, answer download, sync) like
+    `inclusive_h2d_key_d2h_answer`; beside it the same queries as one runOptimizedDPFTreeQuery
+    call, and as T serialised per-slice engine answers (the round-3 behaviour of the shim)."""
+    import threading
+    from erasurecodedpir_amd import server as S
+    S.setSystemParams(n, efs, 1, 1, 0, 0, 1, 0, 0)  # tree mode, k = 1: p = 2, NUM_ROUNDS = 1
+    sv = S.Server(1, n, efs, 0, T)
+    try:
+        sv.write_rows(np.memmap(shard_path, np.uint8, mode="r"))
+        K = min(K, len(keys))
+        parts = np.zeros((T, 1, efs), np.uint8)
+        cur = {"key": None}
+        start, done = threading.Barrier(T + 1), threading.Barrier(T + 1)
+        stop = []
+
+        def worker(t):
+            while True:
+                start.wait()
+                if stop:
+                    return
+                parts[t] = sv.runOptimizedDPFTreeQueryThread(cur["key"], t, T)
+                done.wait()
+
+        ths = [threading.Thread(target=worker, args=(t,), daemon=True) for t in range(T)]
+        for th in ths:
+            th.start()
+
+        def query(k):
+            cur["key"] = k
+            start.wait()
+            done.wait()
+            return S.assemblDPFTreeQueryThreadResults(sv, parts)
+
+        got = query(keys[0])  # engine creation + the 16 GiB upload + warm-up
+        query(keys[1 % len(keys)])
+        t0 = time.perf_counter()
+        outs = [query(keys[q]) for q in range(K)]
+        thr_ms = (time.perf_counter() - t0) / K * 1e3
+        stop.append(1)
+        start.wait()
+        for th in ths:
+            th.join(10)
+        ok = all(np.array_equal(outs[q], want[q]) for q in range(K))
+        ok &= bool(np.array_equal(got, want[0]))
+        sv.runOptimizedDPFTreeQuery(keys[0], 1)
+        t0 = time.perf_counter()
+        whole = [sv.runOptimizedDPFTreeQuery(keys[q], 1) for q in range(K)]
+        one_ms = (time.perf_counter() - t0) / K * 1e3
+        ok_one = all(np.array_equal(whole[q], want[q]) for q in range(K))
+    finally:
+        sv.freeServer()
+    # the round-3 shim: T per-slice engine answers one after another (each its own descent,
+    # tile-0 latency, reduce and sync)
+    Ks = min(3, K)
+    eng.answer_slice(keys[0], 0, T)
+    t0 = time.perf_counter()
+    ser = [np.bitwise_xor.reduce(np.stack([eng.answer_slice(keys[q], t, T) for t in range(T)]), 0)
+           for q in range(Ks)]
+    ser_ms = (time.perf_counter() - t0) / Ks * 1e3
+    ok_ser = all(np.array_equal(ser[q], want[q]) for q in range(Ks))
+    gib = float(1 << n) * efs / GIB
+    return {"workload": f"the reference call shape (tree.go:60-76) at the north_star shape: 2^{n} x {efs} B, "
+                        f"p=2, T={T} concurrent runOptimizedDPFTreeQueryThread calls per query "
+                        "+ assemblDPFTreeQueryThreadResults (tree.go:60-76)",
+            "threads": T, "steps": K, "ms_per_query": r5(thr_ms),
+            "value": round(gib / (thr_ms / 1e3), 3), "unit": "GiB/s",
+            "one_call_ms_per_query": r5(one_ms),
+            "ratio_vs_one_call": round(thr_ms / one_ms, 4),
+            "serialised_per_slice_ms_per_query": r5(ser_ms),
+            "note": "host-buffer API through the pir_server.h shim (key upload, answer download, "
+                    "sync, Python threads); one_call = runOptimizedDPFTreeQuery on the same "
+                    "server; serialised_per_slice = T pir_engine_answer_slice calls in a row "
+                    "(the shim's round-3 behaviour)",
+            "parity": {"assembled_equals_device_answer": bool(ok),
+                       "one_call_equals_device_answer": bool(ok_one),
+                       "serialised_slices_equal": bool(ok_ser)}}
 
 
 def run_coefs(args, ctx, config):

@@ -79,6 +79,9 @@ PROTOTYPES = {
     "pir_engine_get_shard": (_I, [_P, _U64, _U64, _P]),
     "pir_engine_answer": (_I, [_P, _P, _P]),
     "pir_engine_answer_slice": (_I, [_P, _P, _I, _I, _P]),
+    "pir_engine_answer_slices": (_I, [_P, _P, _I, _P]),
+    "pir_engine_answer_slices_dev": (_I, [_P, _P, _I, _P, _P]),
+    "pir_engine_fold_gathered_dev": (_I, [_P, _P, _I, ctypes.c_uint64, _P, _P]),
     "pir_engine_eval_all": (_I, [_P, _P, _P]),
     "pir_engine_answer_coefs": (_I, [_P, ctypes.POINTER(_P), _U64, _U64, _P]),
     "pir_engine_answer_coefs_dev": (_I, [_P, _P, _U64, _U64, _U64, _P, _P]),
@@ -187,6 +190,8 @@ PROTOTYPES = {
     "assembleWoodruffResponses": (None, [ctypes.POINTER(CClient), _P, _P, _P, _P]),
     "pirSetDevice": (None, [_I]),
     "pirServerShardChanged": (None, [ctypes.POINTER(CServer)]),
+    "pirServerSetRows": (None, [ctypes.POINTER(CServer), ctypes.c_void_p, ctypes.c_uint64,
+                                ctypes.c_uint64, ctypes.c_uint32]),
 }
 
 GLOBALS_INT = ["NUM_PARTIES", "NUM_FILES", "NUM_ENCODED_FILES", "LOG_NUM_ENCODED_FILES",

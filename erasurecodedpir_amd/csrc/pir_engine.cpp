@@ -67,13 +67,6 @@ ncclResult_t rccl_settle(ncclComm_t comm, ncclResult_t r, double timeout_s) {
   return r;
 }
 
-#define RCCL_CALL(comm, expr)                                                                 \
-  do {                                                                                        \
-    ncclResult_t _r = rccl_settle((comm), (expr), 60.0);                                       \
-    if (_r != ncclSuccess)                                                                    \
-      return fail(PIR_ECOMM, "%s failed: %s", #expr,                                          \
-                  _r == ncclInProgress ? "timed out after 60 s" : ncclGetErrorString(_r));    \
-  } while (0)
 
 int ilog2_exact(uint64_t v) {
   if (v == 0 || (v & (v - 1))) return -1;
@@ -151,13 +144,17 @@ struct pir_engine {
   // launch); 2 = every workgroup adds its partial to the answer with memory-side atomics
   // (answers of efs % 4 == 0 bytes at 4-byte aligned addresses; else k_reduce)
   int fused_reduce = 0;
-  uint32_t red_gen = 0;  // mode 2: this launch's zeroing flag value (never 0)
+  uint32_t red_gen = 0;  // mode 2: non-zero selects the atomic reduce in k_query
   uint8_t* d_coef_stage = nullptr;  // explicit-coefficient answers: host vectors staged here
   size_t coef_stage_cap = 0;
   uint8_t* d_mpkey = nullptr;       // multiparty DPF keys: host keys / unaligned device keys
   size_t mpkey_cap = 0;
   uint8_t* h_key = nullptr;     // pinned
   uint8_t* h_res = nullptr;     // pinned
+  uint8_t* d_slices = nullptr;  // pir_engine_answer_slices: T x nq x efs partials
+  size_t slices_cap = 0;
+  uint8_t* h_slices = nullptr;  // pinned
+  size_t h_slices_cap = 0;
   std::vector<DevBuf> user;     // pir_engine_alloc_dev
   std::mutex mu;
   uint64_t byz_counter = 0;
@@ -176,6 +173,8 @@ struct pir_engine {
   // RCCL
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  bool comm_failed = false;   // an exchange failed: the communicator was aborted, answers refuse
+  double comm_timeout_s = 60; // $PIR_COMM_TIMEOUT: bound on one exchange's enqueue
 };
 
 namespace {
@@ -217,6 +216,16 @@ int ensure_nodes(pir::NodeBufs* nb, uint64_t* cap, uint64_t nodes, int nbuf) {
     HIP_TRY(hipMalloc(&nb->t[i], nodes * sizeof(uint32_t)));
   }
   *cap = nodes;
+  return PIR_OK;
+}
+
+int ensure_host(uint8_t** p, size_t* cap, size_t bytes) {  // pinned host staging
+  if (bytes <= *cap) return PIR_OK;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  HIP_TRY(hipHostMalloc(p, bytes));
+  *cap = bytes;
   return PIR_OK;
 }
 
@@ -297,23 +306,27 @@ int ensure_qcnt(pir_engine* e, int nk, hipStream_t s) {
 
 // one launch: key parse, tree and scan of nk queued keys (key_len apart) in k_query; then the
 // slab reduce of all nk answers (d_out: nk x nq x efs)
+// nslices > 1 (a power of two <= 2^qp.lr, nk == 1): d_out gets the nslices partial answers
+// over equal consecutive row ranges instead of the whole answer (runOptimizedDPFTreeQueryThread
+// for every thread of a query at once: the slices are runs of k_query's region slabs)
 int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, int nk,
                  int log_parts_total, uint64_t prefix, uint64_t row0, uint8_t* d_out,
-                 hipStream_t s) {
+                 hipStream_t s, int nslices = 1) {
   const auto& c = e->cfg;
   const pir::ScanShape& sh = qp.shape;
   int rc = ensure_slabs(e, (size_t)nk * pir::query_slab_bytes(qp));
   if (!rc) rc = ensure_buf(&e->d_qscratch, &e->qscratch_cap, pir::query_scratch_bytes(qp));
-  // mode 2 needs whole answer words at aligned addresses; otherwise k_reduce
-  const int fred = e->fused_reduce == 2 && (c.record_bytes % 4 != 0 ||
-                                            reinterpret_cast<uintptr_t>(d_out) % 4 != 0)
+  // mode 2 needs whole answer words at aligned addresses; otherwise k_reduce (always for slices)
+  const int fred = nslices > 1 || (e->fused_reduce == 2 && (c.record_bytes % 4 != 0 ||
+                                            reinterpret_cast<uintptr_t>(d_out) % 4 != 0))
                        ? 0 : e->fused_reduce;
   if (!rc && fred) rc = ensure_qcnt(e, nk, s);
   if (rc) return rc;
   uint32_t gen = 0;
-  if (fred == 2) {
+  if (fred == 2) {  // the workgroups XOR into zeroed answers
     if (++e->red_gen == 0) ++e->red_gen;
     gen = e->red_gen;
+    HIP_TRY(hipMemsetAsync(d_out, 0, (size_t)nk * c.num_rounds * c.record_bytes, s));
   }
   e->last_chunks = 1;
   e->last_fused = 2;
@@ -333,7 +346,7 @@ int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, 
     HIP_TRY(hipEventRecord(ev[EV_SCAN_E], s));
     HIP_TRY(hipEventRecord(ev[EV_PRERED], s));
   }
-  if (!fred) HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, d_out, s, nk));
+  if (!fred) HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, d_out, s, nk, nslices));
   if (ev) HIP_TRY(hipEventRecord(ev[EV_RED], s));
   return PIR_OK;
 }
@@ -410,9 +423,17 @@ int answer_batch_core(pir_engine* e, const uint8_t* d_raw, int nk, int log_parts
   e->last_fused = 0;
   e->last_chunks = 1;
   const pir::TreePlan pl = pir::make_plan(c.log_num_records, log_parts_total, prefix, e->batch_k_last, c.num_parties, 8);
-  const pir::ScanShape sh =
+  pir::ScanShape sh =
       pir::make_scan_shape(pl.nleaves, e->pitch, W, e->num_cus, e->batch_scan_bpc);
   const size_t cb_bytes = (size_t)pl.nleaves * W;
+  // k_scan_t reads the group's shares key-major (key g's nrp bytes of leaf i at g * nleaves *
+  // nrp + i * nrp), so each tree's leaf stage writes its shares contiguously (packed 16-byte
+  // stores); the other scans read them interleaved per record (cb[i][W], key g at g * nrp)
+  const bool kmaj = sh.tfold && !(getenv("PIR_BATCH_KMAJOR") && atoi(getenv("PIR_BATCH_KMAJOR")) == 0);
+  if (kmaj) {
+    sh.ckey = (uint32_t)e->nrp;
+    sh.ckoff = (uint64_t)pl.nleaves * e->nrp;
+  }
   // super-group: as many keys as kBatchNodeBytes of upper-level nodes hold (a multiple of G)
   const uint64_t per_key = 2 * pl.max_nodes * (sizeof(uint4) + sizeof(uint32_t));
   int FB = (int)std::min<uint64_t>(kFrontBatch, std::max<uint64_t>(1, kBatchNodeBytes / per_key));
@@ -447,9 +468,10 @@ int answer_batch_core(pir_engine* e, const uint8_t* d_raw, int nk, int log_parts
     const uint64_t off = (uint64_t)r0 * pl.max_nodes;
     const pir::NodeBufs nbg{{e->bnodes.s[0] + off, e->bnodes.s[1] + off},
                             {e->bnodes.t[0] + off, e->bnodes.t[1] + off}};
-    const pir::StageBatch sb{ng, pl.max_nodes, (uint32_t)e->nrp, nullptr, nullptr, 0};
-    HIP_TRY(pir::launch_stages(pl, e->d_keys + q0, nbg, 0, 1, cb, e->nrp, s, last, last + 1, W,
-                               &sb));
+    const pir::StageBatch sb{ng, pl.max_nodes, kmaj ? (uint32_t)sh.ckoff : (uint32_t)e->nrp,
+                             nullptr, nullptr, 0};
+    HIP_TRY(pir::launch_stages(pl, e->d_keys + q0, nbg, 0, 1, cb, e->nrp, s, last, last + 1,
+                               kmaj ? e->nrp : W, &sb));
     HIP_TRY(hipEventRecord(e->ev_cb_ready[b], s));
     HIP_TRY(hipStreamWaitEvent(e->aux, e->ev_cb_ready[b], 0));
     // slots g >= ng hold stale shares: their rounds are computed and dropped
@@ -472,8 +494,44 @@ int answer_batch_core(pir_engine* e, const uint8_t* d_raw, int nk, int log_parts
 
 int check_key_ptr(const void* p) { return p ? PIR_OK : fail(PIR_EINVAL, "null key"); }
 
+// The split-shard combine after the all-gather: d_gather holds nranks blocks of `bytes`
+// (rank r's partial answers at r * bytes -- ncclAllGather's layout), d_result[i] = XOR_r of
+// them (the XOR assembly of server.cpp:553-562 across partitions; RCCL has no XOR op).
+int fold_gathered(pir_engine* e, const uint8_t* d_gather, int nranks, size_t bytes,
+                  uint8_t* d_result, hipStream_t s) {
+  (void)e;
+  HIP_TRY(pir::launch_xor_fold(d_gather, nranks, bytes, d_result, s));
+  return PIR_OK;
+}
+
+// Every rank's `bytes` of partial answers (d_part) -> every rank's XOR over ranks (d_result):
+// ONE ncclAllGather into d_gather (nranks x bytes) + fold_gathered, on stream s.  A failed or
+// timed-out exchange aborts the communicator (an operation may still be in flight on it) and
+// marks the engine failed, so that later answers refuse instead of returning partition-only
+// partials.
+int exchange(pir_engine* e, const uint8_t* d_part, size_t bytes, uint8_t* d_gather,
+             uint8_t* d_result, hipStream_t s) {
+  const ncclResult_t r = rccl_settle(
+      e->comm, ncclAllGather(d_part, d_gather, bytes, ncclUint8, e->comm, s), e->comm_timeout_s);
+  if (r != ncclSuccess) {
+    (void)ncclCommAbort(e->comm);
+    e->comm = nullptr;
+    e->comm_failed = true;
+    return fail(PIR_ECOMM, "ncclAllGather of %zu bytes failed: %s (communicator aborted)", bytes,
+                r == ncclInProgress ? "timed out" : ncclGetErrorString(r));
+  }
+  return fold_gathered(e, d_gather, e->nranks, bytes, d_result, s);
+}
+
+int check_comm(const pir_engine* e) {
+  return e->comm_failed ? fail(PIR_ECOMM, "the engine's communicator was aborted after a failed "
+                                          "exchange (%s)", "re-create the engine")
+                        : PIR_OK;
+}
+
 // before an answer on stream s: order it after the previous answer's use of the workspace
 int ws_acquire(pir_engine* e, hipStream_t s) {
+  if (int rc = check_comm(e)) return rc;
   if (e->ws_stream && e->ws_stream != s) HIP_TRY(hipStreamWaitEvent(s, e->ev_ws, 0));
   return PIR_OK;
 }
@@ -550,8 +608,7 @@ int answer_dev_locked(pir_engine* e, const uint8_t* d_key, uint8_t* d_result, hi
                        part_out, s);
   if (rc) return rc;
   if (e->comm) {
-    RCCL_CALL(e->comm, ncclAllGather(e->d_part, e->d_gather, out_bytes, ncclUint8, e->comm, s));
-    HIP_TRY(pir::launch_xor_fold(e->d_gather, e->nranks, out_bytes, d_result, s));
+    if (int rc = exchange(e, e->d_part, out_bytes, e->d_gather, d_result, s)) return rc;
   }
   if (ev) HIP_TRY(hipEventRecord(ev[EV_END], s));
   e->ev = nullptr;
@@ -587,8 +644,7 @@ int answer_batch_locked(pir_engine* e, const uint8_t* d_keys, int nk, uint8_t* d
                              part_out, s);
   if (rc) return rc;
   if (e->comm) {
-    RCCL_CALL(e->comm, ncclAllGather(e->d_bpart, e->d_bgather, total, ncclUint8, e->comm, s));
-    HIP_TRY(pir::launch_xor_fold(e->d_bgather, e->nranks, total, d_result, s));
+    if (int rc = exchange(e, e->d_bpart, total, e->d_bgather, d_result, s)) return rc;
   }
   return PIR_OK;
 }
@@ -630,11 +686,46 @@ int answer_stream_locked(pir_engine* e, const uint8_t* d_keys, int nk, uint8_t* 
                         part_out, s);
   if (rc) return rc;
   if (e->comm) {
-    RCCL_CALL(e->comm, ncclAllGather(e->d_bpart, e->d_bgather, total, ncclUint8, e->comm, s));
-    HIP_TRY(pir::launch_xor_fold(e->d_bgather, e->nranks, total, d_result, s));
+    if (int rc = exchange(e, e->d_bpart, total, e->d_bgather, d_result, s)) return rc;
   }
   if (e->ev) HIP_TRY(hipEventRecord(e->ev[EV_END], s));
   e->ev = nullptr;
+  return PIR_OK;
+}
+
+// Every slice of one query: d_result[t] (t < 2^lt, num_rounds x record_bytes each) = the
+// partial answer over this engine's rows [t*R/2^lt, (t+1)*R/2^lt) -- what the T calls
+// runOptimizedDPFTreeQueryThread(t, T) of one query return (server.cpp:505-549, intended
+// semantics; tree.go:60-76 issues them concurrently with the same key).  One k_query launch over
+// the whole shard when its 2^lr regions split evenly into the slices (one tree, one pass, a
+// slab reduce per run of regions); else one answer per slice.  Partials stay per engine: no
+// all-gather (the Thread form has none either).
+int answer_slices_locked(pir_engine* e, const uint8_t* d_key, int lt, uint8_t* d_result,
+                         hipStream_t s) {
+  const auto& c = e->cfg;
+  const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
+  const int T = 1 << lt;
+  e->ev = nullptr;
+  const pir::QueryPlan qp = pir::make_query_plan(c.log_num_records, c.log_num_partitions,
+                                                 c.num_parties, c.num_rounds, e->pitch, e->num_cus);
+  if (qp.tile && lt <= qp.lr && e->allow_query && e->allow_fused)
+    return answer_query(e, qp, d_key, 1, c.log_num_partitions, (uint64_t)c.partition_index, 0,
+                        d_result, s, T);
+  for (int t = 0; t < T; ++t) {
+    const uint64_t prefix = ((uint64_t)c.partition_index << lt) | (uint64_t)t;
+    const uint64_t row0 = (uint64_t)t * (e->rows >> lt);
+    int rc = answer_core(e, d_key, c.log_num_partitions + lt, prefix, row0,
+                         d_result + (size_t)t * out_bytes, s);
+    if (rc) return rc;
+  }
+  return PIR_OK;
+}
+
+int check_slices(const pir_engine* e, int num_threads, int* lt) {
+  *lt = ilog2_exact((uint64_t)(num_threads > 0 ? num_threads : 0));
+  if (*lt < 0 || e->cfg.log_num_partitions + *lt > e->cfg.log_num_records)
+    return fail(PIR_EINVAL, "num_threads %d must be a power of two <= 2^%d", num_threads,
+                e->cfg.log_num_records - e->cfg.log_num_partitions);
   return PIR_OK;
 }
 
@@ -659,8 +750,7 @@ int answer_coefs_locked(pir_engine* e, const uint8_t* src, uint64_t pitch, uint6
     HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, out, s));
   }
   if (e->comm) {
-    RCCL_CALL(e->comm, ncclAllGather(e->d_part, e->d_gather, out_bytes, ncclUint8, e->comm, s));
-    HIP_TRY(pir::launch_xor_fold(e->d_gather, e->nranks, out_bytes, d_result, s));
+    if (int rc = exchange(e, e->d_part, out_bytes, e->d_gather, d_result, s)) return rc;
   }
   return PIR_OK;
 }
@@ -692,8 +782,7 @@ int answer_mp_locked(pir_engine* e, const pir::MpLayout& L, const uint8_t* d_key
     HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, out, s));
   }
   if (e->comm) {
-    RCCL_CALL(e->comm, ncclAllGather(e->d_part, e->d_gather, out_bytes, ncclUint8, e->comm, s));
-    HIP_TRY(pir::launch_xor_fold(e->d_gather, e->nranks, out_bytes, d_result, s));
+    if (int rc = exchange(e, e->d_part, out_bytes, e->d_gather, d_result, s)) return rc;
   }
   return PIR_OK;
 }
@@ -836,6 +925,8 @@ void pir_engine_destroy(pir_engine_t* e) {
   for (auto& b : e->user) (void)hipFree(b.p);
   if (e->h_key) (void)hipHostFree(e->h_key);
   if (e->h_res) (void)hipHostFree(e->h_res);
+  if (e->h_slices) (void)hipHostFree(e->h_slices);
+  if (e->d_slices) (void)hipFree(e->d_slices);
   for (auto& sl : e->prof)
     for (auto& ev : sl.ev) (void)hipEventDestroy(ev);
   for (auto& ev : e->ev_leaf)
@@ -1190,6 +1281,43 @@ int pir_engine_answer_slice(pir_engine_t* e, const uint8_t* key, int thread_num,
   return PIR_OK;
 }
 
+int pir_engine_answer_slices_dev(pir_engine_t* e, const uint8_t* d_key, int num_threads,
+                                 uint8_t* d_results, void* stream) {
+  if (!e || !d_results) return fail(PIR_EINVAL, "null argument");
+  if (int rc = check_key_ptr(d_key)) return rc;
+  int lt = 0;
+  if (int rc = check_slices(e, num_threads, &lt)) return rc;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  if (int rc = ws_acquire(e, s)) return rc;
+  return ws_release(e, s, answer_slices_locked(e, d_key, lt, d_results, s));
+}
+
+int pir_engine_answer_slices(pir_engine_t* e, const uint8_t* key, int num_threads,
+                             uint8_t* results) {
+  if (!e || !results) return fail(PIR_EINVAL, "null argument");
+  if (int rc = check_key_ptr(key)) return rc;
+  int lt = 0;
+  if (int rc = check_slices(e, num_threads, &lt)) return rc;
+  const auto& c = e->cfg;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(c.device));
+  const size_t bytes = (size_t)num_threads * c.num_rounds * c.record_bytes;
+  if (int rc = ws_acquire(e, e->stream)) return rc;
+  if (int rc = ensure_buf(&e->d_slices, &e->slices_cap, bytes)) return rc;
+  if (int rc = ensure_host(&e->h_slices, &e->h_slices_cap, bytes)) return rc;
+  memcpy(e->h_key, key, e->key_len);
+  HIP_TRY(hipMemcpyAsync(e->d_key_raw, e->h_key, e->key_len, hipMemcpyHostToDevice, e->stream));
+  int rc = ws_release(e, e->stream, answer_slices_locked(e, e->d_key_raw, lt, e->d_slices,
+                                                         e->stream));
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(e->h_slices, e->d_slices, bytes, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memcpy(results, e->h_slices, bytes);
+  return PIR_OK;
+}
+
 int pir_engine_eval_all(pir_engine_t* e, const uint8_t* key, uint8_t* out) {
   if (!e || !out) return fail(PIR_EINVAL, "null argument");
   if (int rc = check_key_ptr(key)) return rc;
@@ -1392,6 +1520,15 @@ int pir_engine_get_shard(pir_engine_t* e, uint64_t row0, uint64_t nrows, uint8_t
   return PIR_OK;
 }
 
+int pir_engine_fold_gathered_dev(pir_engine_t* e, const uint8_t* d_gathered, int nranks,
+                                 uint64_t bytes_per_rank, uint8_t* d_result, void* stream) {
+  if (!e || !d_gathered || !d_result || nranks < 1) return fail(PIR_EINVAL, "bad argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  return fold_gathered(e, d_gathered, nranks, (size_t)bytes_per_rank, d_result, s);
+}
+
 int pir_comm_unique_id(uint8_t id[PIR_COMM_ID_BYTES]) {
   static_assert(sizeof(ncclUniqueId) == PIR_COMM_ID_BYTES, "ncclUniqueId size");
   ncclUniqueId u;
@@ -1427,6 +1564,9 @@ int pir_comm_attach(pir_engine_t* e, const uint8_t id[PIR_COMM_ID_BYTES], int nr
   e->comm = comm;
   e->nranks = nranks;
   e->rank = rank;
+  e->comm_failed = false;
+  const char* xt = getenv("PIR_COMM_TIMEOUT");  // seconds one exchange may take to enqueue
+  if (xt && atof(xt) > 0) e->comm_timeout_s = atof(xt);
   HIP_TRY(hipMalloc(&e->d_gather, (size_t)nranks * e->cfg.num_rounds * e->cfg.record_bytes));
   return PIR_OK;
 }

@@ -119,6 +119,11 @@ struct ScanShape {
   dim3 grid;
   int threads;           // k_scan_uni workgroup: kScanThreads, or kScanM4rThreads (4-5 rounds)
   bool tfold;            // k_scan_t (pir_scan_t.hip): transposed four-Russians fold, VEC = 1
+  // k_scan_t only: coefficients key-major (batched answers): ckey bytes per key and record, key
+  // g's block at g * ckoff (record i's word = the NRP / ckey keys' ckey bytes, key g at byte
+  // g * ckey); ckey == 0: record-major, record i's NRP bytes at i * NRP
+  uint32_t ckey = 0;
+  uint64_t ckoff = 0;
 };
 // k_scan_t takes 4-8 rounds of 4/8 coefficient bytes per record over records of >= 256 B
 // ($PIR_SCAN_T=0: the k_scan_uni forms instead).  Workgroups of kScanTThreads, kScanTBlocksPerCU
@@ -175,16 +180,19 @@ size_t query_scratch_bytes(const QueryPlan& qp);
 // out != nullptr: the answers are reduced in-kernel (no launch_reduce): query k's nq x efs bytes
 // at out + k * nq * efs.  gen == 0: qcnt = nk zeroed counters (the kernel leaves them zero),
 // the last workgroup reduces; gen != 0: every workgroup adds its partial with memory-side
-// atomics, qcnt[0] = the launch's zeroing flag (gen unique per launch; efs % 4 == 0)
+// atomics into answers the host zeroed before the launch (efs % 4 == 0)
 hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
                         int p, int n, int party0, int log_parts, uint64_t prefix,
                         const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
                         uint64_t* trace = nullptr, uint8_t* out = nullptr,
                         uint32_t* qcnt = nullptr, uint32_t efs = 0, uint32_t gen = 0);
 // XOR the slabs, compact pitch -> record_bytes: d_out[a*efs + b]; nk queries (slabs of query k
-// grid.x*grid.y*slab_bytes apart, answers nq*efs bytes apart)
+// grid.x*grid.y*slab_bytes apart, answers nq*efs bytes apart).  nslices > 1 (dividing grid.x):
+// per query, nslices answers over consecutive equal runs of the grid.x slabs, i.e. over equal
+// consecutive row ranges when slab x covers rows [x*R, (x+1)*R) (k_query); answer (k, z) at
+// d_out + (k*nslices + z)*nq*efs.
 hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t efs,
-                         uint8_t* d_out, hipStream_t s, int nk = 1);
+                         uint8_t* d_out, hipStream_t s, int nk = 1, int nslices = 1);
 // d_out[i] = XOR_r d_in[r*len + i]
 hipError_t launch_xor_fold(const uint8_t* d_in, int nranks, size_t len, uint8_t* d_out,
                            hipStream_t s);

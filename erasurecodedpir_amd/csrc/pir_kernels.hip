@@ -1238,8 +1238,8 @@ __global__ __launch_bounds__(NT) void k_query(
   // out != nullptr: the slabs of each query are reduced in-kernel into out (query k at
   // out + k * nq * efs); else the host launches k_reduce.  red_gen == 0: the last workgroup to add
   // to qcnt[k] (zero on entry, left zero) XORs every slab.  red_gen != 0 (efs % 4 == 0, out 4-byte
-  // aligned): every workgroup XORs its partial answer into out with memory-side atomics, after
-  // workgroup 0 has zeroed out (stores past L2) and published red_gen in qcnt[0] -- no slab
+  // aligned): every workgroup XORs its partial answer into out with memory-side atomics; the
+  // host zeroes out (hipMemsetAsync on the launch's stream) before the launch -- no slab
   // traffic and no single-workgroup tail.
   // trace != nullptr: per-workgroup wall-clock stamps (100 MHz) of query 0's phases,
   // kQueryTraceSlots apart (layout: pir_engine_trace_query, include/pir_engine.h)
@@ -1265,19 +1265,10 @@ __global__ __launch_bounds__(NT) void k_query(
     sm.bar = 0; sm.sbar = 0; sm.ready = 0;
     for (int r = 0; r < RING; ++r) sm.consumed[r] = 0;
   }
+  // atomic_red: the answers were zeroed by a memset the host enqueued before this launch (on
+  // the same stream), so no workgroup waits on another's progress
   const bool atomic_red = out && red_gen;
-  if (atomic_red && blockIdx.x == 0) {  // zero every queued answer, past this XCD's L2
-    uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
-    const uint32_t words = (uint32_t)nk * NQ * (efs / 4);
-    for (uint32_t i = threadIdx.x; i < words; i += NT)
-      __hip_atomic_store(o32 + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  }
   __syncthreads();
-  if (atomic_red && blockIdx.x == 0 && threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_store(qcnt, red_gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
   if (trace && threadIdx.x == 0) trace[1] = wall_clock64();
 
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1769,13 +1760,7 @@ __global__ __launch_bounds__(NT) void k_query(
         uint32_t* qslab = reinterpret_cast<uint32_t*>(slabs) + qy * slab_q_words;
         const int st = (int)threadIdx.x - TW * 64;
         if (atomic_red) {
-          // the workgroup's partial answer straight into out (memory-side atomics), once
-          // workgroup 0's zeros are published (long done by now: a wait that never spins)
-          if (st == 0)
-            while (__hip_atomic_load(qcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != red_gen)
-              __builtin_amdgcn_s_sleep(2);
-          group_barrier(&sm.sbar, sgen, SW);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          // the workgroup's partial answer straight into the zeroed out (memory-side atomics)
           uint32_t* o32 = reinterpret_cast<uint32_t*>(out + (size_t)qy * NQ * efs);
           const uint32_t wpr = efs / 4;  // answer words per round
           for (uint32_t gg = 0; gg < gy; ++gg)
@@ -1851,16 +1836,21 @@ __global__ __launch_bounds__(NT) void k_query(
   }
 }
 
-// slabs: [grid.y][grid.x][nq][GW words]; out[a*efs + b] for b < efs.
+// slabs: [grid.y][gx_all][nq][GW words]; out[a*efs + b] for b < efs.
 // One 1024-thread block per 64 output words: 16 lane groups split the gx slabs, then LDS.
-// blockIdx.y = query of a queue: slabs q_words apart, answers nq*efs bytes apart.
+// blockIdx.y = query of a queue: slabs q_words apart, answers gridDim.z*nq*efs bytes apart.
+// blockIdx.z = slice: the slabs [z*gx, (z+1)*gx) of gx_all = gridDim.z*gx (k_query's workgroup
+// b owns rows [b*R, (b+1)*R), so slice z of gridDim.z is the partial answer over the rows
+// [z*N/Z, (z+1)*N/Z) -- runOptimizedDPFTreeQueryThread's slice, server.cpp:519-541),
+// answer (y, z) at out + (y*gridDim.z + z)*nq*efs.
 __global__ __launch_bounds__(kReduceThreads) void k_reduce(const uint32_t* __restrict__ slabs,
                                                            int nq, uint32_t gw, uint32_t gx,
                                                            uint32_t pitch, uint32_t efs,
                                                            uint8_t* __restrict__ out,
                                                            uint64_t q_words) {
-  slabs += blockIdx.y * q_words;
-  out += (uint64_t)blockIdx.y * nq * efs;
+  const uint32_t gx_all = gx * gridDim.z;
+  slabs += blockIdx.y * q_words + (uint64_t)blockIdx.z * gx * nq * gw;
+  out += ((uint64_t)blockIdx.y * gridDim.z + blockIdx.z) * nq * efs;
   __shared__ uint32_t part[kReduceThreads / 64][64];
   const uint32_t words = pitch / 4;
   const uint32_t lane = threadIdx.x & 63, grp16 = threadIdx.x >> 6, ngrp = blockDim.x >> 6;
@@ -1869,7 +1859,7 @@ __global__ __launch_bounds__(kReduceThreads) void k_reduce(const uint32_t* __res
   if (idx < (uint32_t)nq * words) {
     const uint32_t a = idx / words, w = idx - a * words;
     const uint32_t grp = w / gw, win = w - grp * gw;
-    const uint32_t* p = slabs + ((uint64_t)grp * gx) * nq * gw + (uint64_t)a * gw + win;
+    const uint32_t* p = slabs + ((uint64_t)grp * gx_all) * nq * gw + (uint64_t)a * gw + win;
     const uint64_t stride = (uint64_t)nq * gw;
     uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     uint32_t x = grp16;
@@ -2515,14 +2505,15 @@ hipError_t launch_scan(const ScanShape& sh, const uint8_t* d_shard, uint64_t nre
 }
 
 hipError_t launch_reduce(const ScanShape& sh, const uint8_t* d_slabs, uint32_t efs,
-                         uint8_t* d_out, hipStream_t s, int nk) {
+                         uint8_t* d_out, hipStream_t s, int nk, int nslices) {
   const uint32_t words = sh.pitch / 4;
   const uint32_t total = (uint32_t)sh.nq * words;
   const uint32_t gw = kColGroupLanes * sh.vec;
   const uint64_t q_words = (uint64_t)sh.grid.x * sh.grid.y * (sh.slab_bytes / 4);
-  hipLaunchKernelGGL(k_reduce, dim3((total + 63) / 64, nk), dim3(kReduceThreads), 0, s,
-                     reinterpret_cast<const uint32_t*>(d_slabs), sh.nq, gw, sh.grid.x,
-                     sh.pitch, efs, d_out, q_words);
+  if (nslices < 1 || sh.grid.x % (uint32_t)nslices != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_reduce, dim3((total + 63) / 64, nk, nslices), dim3(kReduceThreads), 0, s,
+                     reinterpret_cast<const uint32_t*>(d_slabs), sh.nq, gw,
+                     sh.grid.x / (uint32_t)nslices, sh.pitch, efs, d_out, q_words);
   return hipGetLastError();
 }
 

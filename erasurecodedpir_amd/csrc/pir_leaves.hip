@@ -65,11 +65,29 @@ struct DfsOut {
   uint32_t* t;
 };
 
+// Packed leaf stores (PACK: leaf i's NRP bytes at c + i * NRP, i.e. one key's shares
+// contiguous -- the key-major share layout of batched answers, or a single key): the DFS emits
+// a lane's leaves in increasing index order, so they shift into a 16-byte register (newest at
+// the top) and every 16 / NRP leaves leave as ONE 16-byte store, instead of a 1-4 byte store
+// per leaf (2.25 GB written per 8-key launch for 128 MiB of shares, r03_pmc_c3b.json).
+template <int NRP>
+__device__ __forceinline__ void pack_leaf(uint4& acc, uint32_t v) {
+  constexpr int SH = 8 * NRP;  // bits per leaf (NRP <= 4)
+  if constexpr (SH == 32) {
+    acc = make_uint4(acc.y, acc.z, acc.w, v);
+  } else {
+    acc.x = __builtin_amdgcn_alignbit(acc.y, acc.x, SH);
+    acc.y = __builtin_amdgcn_alignbit(acc.z, acc.y, SH);
+    acc.z = __builtin_amdgcn_alignbit(acc.w, acc.z, SH);
+    acc.w = __builtin_amdgcn_alignbit(v, acc.w, SH);
+  }
+}
+
 // the 2^D leaves (or bottom nodes) under node (s, t) of level L, indices [i0, i0 + 2^D)
-template <bool NODES, int NRP, int TB, int D>
+template <bool NODES, int NRP, int TB, int D, bool PACK>
 __device__ __forceinline__ void subtree_dfs(const Tab4& T, const DevKey* __restrict__ K, int L,
                                             const Bits& B, uint4 s, uint32_t t, uint64_t i0,
-                                            const DfsOut& o) {
+                                            const DfsOut& o, uint4& acc) {
   uint4 sl, sr;
   uint32_t tl, tr;
   expand_node4<TB>(T, K, L, B, s, t, sl, sr, tl, tr);
@@ -80,21 +98,29 @@ __device__ __forceinline__ void subtree_dfs(const Tab4& T, const DevKey* __restr
     } else {
       const uint4 vl = leaf_value4<NRP>(T, K, B.pm1, sl, tl);
       const uint4 vr = leaf_value4<NRP>(T, K, B.pm1, sr, tr);
-      store_leaf<NRP>(o.c, i0, and_q(vl, o.qm), o.cstride);
-      store_leaf<NRP>(o.c, i0 + 1, and_q(vr, o.qm), o.cstride);
+      if constexpr (PACK) {
+        constexpr uint32_t LPS = 16 / NRP;  // leaves per 16-byte store
+        pack_leaf<NRP>(acc, vl.x & o.qm.x);
+        pack_leaf<NRP>(acc, vr.x & o.qm.x);
+        if (((uint32_t)i0 & (LPS - 1)) == LPS - 2)  // leaf i0 + 1 completes the register
+          *reinterpret_cast<uint4*>(o.c + (i0 + 2 - LPS) * NRP) = acc;
+      } else {
+        store_leaf<NRP>(o.c, i0, and_q(vl, o.qm), o.cstride);
+        store_leaf<NRP>(o.c, i0 + 1, and_q(vr, o.qm), o.cstride);
+      }
     }
   } else {
     // one copy of the subtree code per level: the right child waits in registers
 #pragma unroll 1
     for (int i = 0; i < 2; ++i)
-      subtree_dfs<NODES, NRP, TB, D - 1>(T, K, L + 1, B, i ? sr : sl, i ? tr : tl,
-                                         i0 + ((uint64_t)i << (D - 1)), o);
+      subtree_dfs<NODES, NRP, TB, D - 1, PACK>(T, K, L + 1, B, i ? sr : sl, i ? tr : tl,
+                                               i0 + ((uint64_t)i << (D - 1)), o, acc);
   }
 }
 
 // blockIdx.y = key of a batch: its DevKey, input node range (in_stride apart) and outputs
 // (shares at c + y * c_key_off, or nodes out_stride apart)
-template <bool NODES, int NRP, int TB, int KD>
+template <bool NODES, int NRP, int TB, int KD, bool PACK = false>
 __global__ __launch_bounds__(kLeafThreads)
 void k_subtree(const DevKey* __restrict__ K, const uint4* __restrict__ in_s,
                const uint32_t* __restrict__ in_t, int L0, uint64_t nin, uint64_t in_stride,
@@ -125,7 +151,8 @@ void k_subtree(const DevKey* __restrict__ K, const uint4* __restrict__ in_s,
   const Tab4 T(tab);
   const uint64_t u = (uint64_t)blockIdx.x * kLeafThreads + threadIdx.x;
   if (u >= nin) return;  // no barrier below
-  subtree_dfs<NODES, NRP, TB, KD>(T, K, L0, B, in_s[u], in_t[u], u << KD, o);
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  subtree_dfs<NODES, NRP, TB, KD, PACK>(T, K, L0, B, in_s[u], in_t[u], u << KD, o, acc);
 }
 
 bool leaves_supported(int kd) { return kd >= kLeavesMinK && kd <= kLeavesMaxK; }
@@ -144,17 +171,31 @@ struct SubtreeArgs {
   uint64_t out_stride;
 };
 
-template <bool NODES, int NRP, int TB, int KD>
+template <bool NODES, int NRP, int TB, int KD, bool PACK = false>
 static hipError_t subtree_launch(dim3 grid, const SubtreeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((k_subtree<NODES, NRP, TB, KD>), grid, dim3(kLeafThreads), 0, s, a.key,
-                     a.is, a.it, a.L0, a.nin, a.in_stride, a.c, a.cstride, a.c_key_off, a.os,
-                     a.ot, a.out_stride);
+  hipLaunchKernelGGL((k_subtree<NODES, NRP, TB, KD, PACK>), grid, dim3(kLeafThreads), 0, s,
+                     a.key, a.is, a.it, a.L0, a.nin, a.in_stride, a.c, a.cstride, a.c_key_off,
+                     a.os, a.ot, a.out_stride);
   return hipGetLastError();
 }
 
 // TB = bytes of the control-bit block the node reads: 2(p-1) bits
 template <int NRP, int TB>
 static hipError_t leaves_kd(int kd, dim3 grid, const SubtreeArgs& a, hipStream_t s) {
+  // contiguous shares of <= 4 bytes at 16-byte aligned subtree bases: packed 16-byte stores
+  // ($PIR_LEAF_PACK=0: one store per leaf, diagnostics)
+  const char* pk = getenv("PIR_LEAF_PACK");
+  const bool pack_ok = !(pk && atoi(pk) == 0);
+  if constexpr (NRP <= 4) {
+    if (pack_ok && a.cstride == (uint32_t)NRP && (reinterpret_cast<uintptr_t>(a.c) & 15) == 0 &&
+        ((uint64_t)a.c_key_off & 15) == 0) {
+      switch (kd) {
+        case 4: return subtree_launch<false, NRP, TB, 4, true>(grid, a, s);
+        case 5: return subtree_launch<false, NRP, TB, 5, true>(grid, a, s);
+        default: return hipErrorInvalidValue;
+      }
+    }
+  }
   switch (kd) {
     case 4: return subtree_launch<false, NRP, TB, 4>(grid, a, s);
     case 5: return subtree_launch<false, NRP, TB, 5>(grid, a, s);

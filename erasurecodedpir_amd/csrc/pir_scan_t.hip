@@ -36,12 +36,14 @@ __device__ __forceinline__ uint32_t gf_xtime4_t(uint32_t x) {  // 4 packed bytes
 template <int NQ, int NRP>
 __global__ __launch_bounds__(kScanTThreads) __attribute__((amdgpu_waves_per_eu(kScanTWavesPerEU)))
 void k_scan_t(const uint8_t* __restrict__ shard, uint64_t nrec, uint32_t pitch, uint32_t cpr,
-              const uint8_t* __restrict__ c, uint8_t* __restrict__ slabs, int accumulate) {
+              const uint8_t* __restrict__ c, uint8_t* __restrict__ slabs, int accumulate,
+              uint32_t ckey, uint64_t ckoff) {
   static_assert(NRP == 4 || NRP == 8, "coefficient words of 32 or 64 bits");
   static_assert(NQ >= 1 && NQ <= NRP, "rounds");
   constexpr int WD = NRP / 4;  // coefficient words per record (rounds 0-3, 4-7)
   constexpr int GW = kColGroupLanes;
-  __shared__ uint32_t tab[kScanTWaves][256 * WD];  // per wave: T[v] at [v * WD]
+  // per wave: T[v] at [v * WD]; read as uint2 (ds_read_b64) when WD == 2, hence 8-aligned
+  __shared__ alignas(8) uint32_t tab[kScanTWaves][256 * WD];
   __shared__ uint32_t red[NQ * GW];
   for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) red[i] = 0;
 
@@ -69,14 +71,28 @@ void k_scan_t(const uint8_t* __restrict__ shard, uint64_t nrec, uint32_t pitch, 
     auto load_rel = [&](uint32_t rel) __attribute__((always_inline)) {
       return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, voff, rel < nrows ? rel * pitch : 0u, 2);
     };
-    // lane l: the coefficient words of row rb + l (zero past the wave's rows)
+    // lane l: the coefficient words of row rb + l (zero past the wave's rows); key-major
+    // coefficients (ckey bytes per key) are gathered key by key: one ckey-byte load per key,
+    // coalesced across the wave's 64 rows
     auto coefs64 = [&](uint32_t rb) __attribute__((always_inline)) {
       const uint32_t rl = rb + lane;
       uint2 cw = make_uint2(0, 0);
       if (rl < nrows) {
-        const uint8_t* p = c + (r0 + rl) * NRP;
-        if constexpr (NRP == 8) cw = *reinterpret_cast<const uint2*>(p);
-        else cw.x = *reinterpret_cast<const uint32_t*>(p);
+        const uint64_t row = r0 + rl;
+        if (ckey == 0) {
+          const uint8_t* p = c + row * NRP;
+          if constexpr (NRP == 8) cw = *reinterpret_cast<const uint2*>(p);
+          else cw.x = *reinterpret_cast<const uint32_t*>(p);
+        } else {
+          uint64_t w = 0;
+          for (uint32_t g = 0; g * ckey < (uint32_t)NRP; ++g) {
+            const uint8_t* p = c + g * ckoff + row * ckey;
+            const uint64_t v = ckey == 1 ? *p : (ckey == 2 ? *reinterpret_cast<const uint16_t*>(p)
+                                                           : *reinterpret_cast<const uint32_t*>(p));
+            w |= v << (8 * g * ckey);
+          }
+          cw = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+        }
       }
       return cw;
     };
@@ -210,8 +226,9 @@ bool scan_t_shape(int nq, int nrp, uint32_t pitch) {
 template <int NQ, int NRP>
 static hipError_t scan_t_launch(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
                                 const uint8_t* d_c, uint8_t* d_slabs, int acc, hipStream_t s) {
+  if (sh.ckey != 0 && (sh.ckey > 4 || NRP % sh.ckey != 0)) return hipErrorInvalidValue;
   hipLaunchKernelGGL((k_scan_t<NQ, NRP>), sh.grid, dim3(kScanTThreads), 0, s, d_shard, nrec,
-                     sh.pitch, sh.cpr, d_c, d_slabs, acc);
+                     sh.pitch, sh.cpr, d_c, d_slabs, acc, sh.ckey, sh.ckoff);
   return hipGetLastError();
 }
 

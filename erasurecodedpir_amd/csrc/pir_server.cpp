@@ -10,6 +10,7 @@
 #include <string.h>
 #include <sys/random.h>
 
+#include <algorithm>
 #include <mutex>
 #include <random>
 #include <utility>
@@ -64,6 +65,19 @@ int device_default() {
   abort();  // the reference's handleErrors() (utils.cpp:11-15)
 }
 
+// The slices of one query, computed together for the T runOptimizedDPFTreeQueryThread calls
+// that tree.go:60-76 issues with the same key: the first call to arrive answers every slice in
+// one engine pass (pir_engine_answer_slices), the others copy theirs out.  An entry lives
+// until each of its T slices has been taken once (or the shard / engine changes).
+struct SliceGroup {
+  std::vector<uint8_t> key;
+  int num_threads = 0;
+  std::vector<uint8_t> parts;   // num_threads x NUM_ROUNDS x efs
+  std::vector<uint8_t> taken;   // per slice
+  int left = 0;
+};
+constexpr size_t kMaxSliceGroups = 8;  // queries whose slices are in flight at once
+
 // Per-server engine state, hung off server.ctx.
 struct ShimState {
   std::mutex mu;
@@ -71,6 +85,8 @@ struct ShimState {
   pir_engine_config cfg{};
   bool dirty = true;  // indexList changed since the last upload
   uint32_t rows_alloc = 0;
+  uint32_t row_bytes = 0;          // bytes per indexList row (initializeServer's fileSizeBytes)
+  std::vector<SliceGroup> groups;  // oldest first
 };
 
 ShimState* state_of(server* s) {
@@ -99,6 +115,7 @@ pir_engine_t* engine_for(server* s, ShimState* st, int nq) {
   c.log_num_partitions = 0;
   c.partition_index = 0;
   c.is_byzantine = s->isByzantine;
+  if (!st->eng || memcmp(&c, &st->cfg, sizeof c) != 0 || st->dirty) st->groups.clear();
   if (!st->eng || memcmp(&c, &st->cfg, sizeof c) != 0) {
     if (st->eng) pir_engine_destroy(st->eng);
     st->eng = nullptr;
@@ -414,6 +431,21 @@ void pirServerShardChanged(server* s) {
   if (s && s->ctx) static_cast<ShimState*>(s->ctx)->dirty = true;
 }
 
+void pirServerSetRows(server* s, const uint8_t* rows, uint64_t row0, uint64_t nrows,
+                      uint32_t rowBytes) {
+  ShimState* st = state_of(s);
+  std::lock_guard<std::mutex> lk(st->mu);
+  if (row0 > st->rows_alloc || nrows > st->rows_alloc - row0 || (!rows && nrows) ||
+      rowBytes > st->row_bytes) {
+    fprintf(stderr, "pir shim: rows [%llu,%llu) outside the server's %u\n",
+            (unsigned long long)row0, (unsigned long long)(row0 + nrows), st->rows_alloc);
+    abort();
+  }
+  for (uint64_t i = 0; i < nrows; ++i)
+    memcpy(s->indexList[row0 + i], rows + i * rowBytes, rowBytes);
+  st->dirty = true;
+}
+
 int calcOptimizedDPFTreeKeyLength(int p, int log_domainSize, int numQueries) {
   return pir_engine_key_len(p, log_domainSize, numQueries);
 }
@@ -492,6 +524,7 @@ void freeParams(void) {}
 void initializeServer(server* s, int partyIndex, uint32_t logNumFiles, uint32_t fileSizeBytes,
                       int isByzantine, int numThreads) {
   auto* st = new ShimState;
+  st->row_bytes = fileSizeBytes;
   s->ctx = st;
   s->ctxThreads = nullptr;
   s->partyIndex = partyIndex;
@@ -526,17 +559,44 @@ void runOptimizedDPFTreeQuery(server* s, uint8_t* key, int numQueries, uint8_t**
   for (int a = 0; a < numQueries; ++a) memcpy(result[a], out.data() + a * efs, efs);
 }
 
-// server.cpp:505-549, intended semantics (see pir_server.h)
+// server.cpp:505-549, intended semantics (see pir_server.h).  The T calls of one query
+// (tree.go:60-76: T goroutines, the same key) share ONE engine pass: the first to take the
+// server lock answers every slice (pir_engine_answer_slices), the rest copy theirs from it.
 void runOptimizedDPFTreeQueryThread(server* s, uint8_t* key, int threadNum, int numThreads,
                                     uint8_t** result) {
   ShimState* st = state_of(s);
   std::lock_guard<std::mutex> lk(st->mu);
   pir_engine_t* e = engine_for(s, st, NUM_ROUNDS);
-  const size_t efs = (size_t)ENCODED_FILE_SIZE_BYTES;
-  std::vector<uint8_t> out((size_t)NUM_ROUNDS * efs);
-  if (pir_engine_answer_slice(e, key, threadNum, numThreads, out.data()) != PIR_OK)
-    die("runOptimizedDPFTreeQueryThread");
-  for (int a = 0; a < NUM_ROUNDS; ++a) memcpy(result[a], out.data() + a * efs, efs);
+  if (!key || numThreads < 1 || threadNum < 0 || threadNum >= numThreads ||
+      (numThreads & (numThreads - 1)) || numThreads > NUM_ENCODED_FILES) {
+    fprintf(stderr, "pir shim: thread %d of %d (a power of two <= %d rows)\n", threadNum,
+            numThreads, NUM_ENCODED_FILES);
+    abort();
+  }
+  const size_t efs = (size_t)ENCODED_FILE_SIZE_BYTES, ans = (size_t)NUM_ROUNDS * efs;
+  const size_t klen = (size_t)calcOptimizedDPFTreeKeyLength(NUM_PARTIES < 2 ? 2 : NUM_PARTIES,
+                                                            LOG_NUM_ENCODED_FILES, NUM_ROUNDS);
+  auto it = std::find_if(st->groups.begin(), st->groups.end(), [&](const SliceGroup& g) {
+    return g.num_threads == numThreads && !g.taken[threadNum] &&
+           memcmp(g.key.data(), key, klen) == 0;
+  });
+  if (it == st->groups.end()) {
+    if (st->groups.size() >= kMaxSliceGroups) st->groups.erase(st->groups.begin());
+    SliceGroup g;
+    g.key.assign(key, key + klen);
+    g.num_threads = numThreads;
+    g.parts.resize((size_t)numThreads * ans);
+    g.taken.assign((size_t)numThreads, 0);
+    g.left = numThreads;
+    if (pir_engine_answer_slices(e, key, numThreads, g.parts.data()) != PIR_OK)
+      die("runOptimizedDPFTreeQueryThread");
+    st->groups.push_back(std::move(g));
+    it = st->groups.end() - 1;
+  }
+  const uint8_t* part = it->parts.data() + (size_t)threadNum * ans;
+  for (int a = 0; a < NUM_ROUNDS; ++a) memcpy(result[a], part + a * efs, efs);
+  it->taken[threadNum] = 1;
+  if (--it->left == 0) st->groups.erase(it);
 }
 
 // server.cpp:553-562 (host buffers from the Go caller)

@@ -177,6 +177,28 @@ class Engine:
               "pir_engine_answer_slice")
         return out
 
+    def answer_slices(self, key, num_threads):
+        """Every thread slice of one query at once, (num_threads, num_rounds, record_bytes):
+        row t = answer_slice(key, t, num_threads) -- the T concurrent
+        runOptimizedDPFTreeQueryThread calls of src/server_util/tree.go:60-76, from one tree and
+        one pass over the shard where the shape allows."""
+        k, kp = self._check_key(key)
+        out = np.empty((num_threads, self.num_rounds, self.record_bytes), np.uint8)
+        check(self._lib.pir_engine_answer_slices(self._h, kp, num_threads,
+                                                 out.ctypes.data_as(ctypes.c_void_p)),
+              "pir_engine_answer_slices")
+        return out
+
+    def answer_slices_dev(self, d_key, num_threads, d_results, stream=None):
+        check(self._lib.pir_engine_answer_slices_dev(self._h, d_key, num_threads, d_results,
+                                                     stream), "answer_slices_dev")
+
+    def fold_gathered_dev(self, d_gathered, nranks, bytes_per_rank, d_result, stream=None):
+        """The split-shard combine after the RCCL all-gather: d_result = XOR over r of the
+        rank-r block of d_gathered (pir_engine_fold_gathered_dev)."""
+        check(self._lib.pir_engine_fold_gathered_dev(self._h, d_gathered, nranks, bytes_per_rank,
+                                                     d_result, stream), "fold_gathered_dev")
+
     def answer_coefs(self, coefs, row0=0, nrows=None):
         """Explicit-coefficient answer (runHollantiQuery[Thread], src/c/server.cpp:321-371):
         coefs is (num_rounds, rows) uint8 -- coefficient of engine row r in round a at

@@ -48,13 +48,12 @@ class Server:
     def partyIndex(self):
         return self.s.partyIndex
 
-    def write_rows(self, rows):
-        """Copy (nrows, file_size) bytes into indexList (as a test harness would) and tell the
-        shim the shard changed."""
+    def write_rows(self, rows, row0=0):
+        """Copy (nrows, file_size) bytes into indexList[row0 ..] (as a test harness would) and
+        mark the shard changed (pirServerSetRows)."""
         rows = np.ascontiguousarray(rows, dtype=np.uint8).reshape(-1, self.file_size)
-        for i in range(rows.shape[0]):
-            ctypes.memmove(self.s.indexList[i], rows[i].ctypes.data, self.file_size)
-        self._lib.pirServerShardChanged(ctypes.byref(self.s))
+        self._lib.pirServerSetRows(ctypes.byref(self.s), rows.ctypes.data, row0, rows.shape[0],
+                                   self.file_size)
 
     def read_row(self, i):
         return np.ctypeslib.as_array(self.s.indexList[i], (self.file_size,)).copy()

@@ -13,6 +13,8 @@
  *   pir_engine_answer                runOptimizedDPFTreeQuery               server.cpp:96-134
  *   pir_engine_answer_slice          runOptimizedDPFTreeQueryThread (intended semantics)
  *                                                                           server.cpp:505-549
+ *   pir_engine_answer_slices[_dev]   the T concurrent ...Thread calls of one query
+ *                                    (src/server_util/tree.go:60-76)        server.cpp:505-549
  *   pir_engine_eval_all              evalAllOptimizedDPF                    dpf_tree.cpp:473-598
  *   pir_engine_answer_coefs[_dev]    runHollantiQuery / ...Thread           server.cpp:321-371
  *   pir_engine_answer_mp[_dev]       runOptimizedMultiPartyDPFQuery[Thread] server.cpp:136-176,
@@ -107,6 +109,15 @@ int pir_engine_answer(pir_engine_t *e, const uint8_t *key, uint8_t *result);
 /* partial answer over the engine rows [t*R/T, (t+1)*R/T), R = rows held, T a power of 2 */
 int pir_engine_answer_slice(pir_engine_t *e, const uint8_t *key, int thread_num,
                             int num_threads, uint8_t *result);
+/* every slice of one query at once: results[t] (t < num_threads, num_rounds * record_bytes
+ * each, back to back) = pir_engine_answer_slice(e, key, t, num_threads, .) -- the T calls of
+ * one query that src/server_util/tree.go:60-76 issues concurrently with the same key
+ * (runOptimizedDPFTreeQueryThread, server.cpp:505-549), computed by ONE tree and ONE pass over
+ * the shard where the shape allows (the pir_server.h shim serves its Thread calls from it) */
+int pir_engine_answer_slices(pir_engine_t *e, const uint8_t *key, int num_threads,
+                             uint8_t *results);
+int pir_engine_answer_slices_dev(pir_engine_t *e, const uint8_t *d_key, int num_threads,
+                                 uint8_t *d_results, void *stream);
 /* ---- explicit-coefficient answers: the Hollanti/Goldberg polynomial-PIR server scan
  *      (runHollantiQuery / runHollantiQueryThread, server.cpp:321-371) -- no DPF, the client
  *      sends one coefficient vector per round ----
@@ -204,8 +215,19 @@ int pir_engine_trace_query(pir_engine_t *e, const uint8_t *d_key, int num_keys, 
 /* ---- split shard across GPUs: XOR all-reduce of partition answers over RCCL ---- */
 #define PIR_COMM_ID_BYTES 128
 int pir_comm_unique_id(uint8_t id[PIR_COMM_ID_BYTES]);
-/* rank r of nranks; nranks must equal 2^G of the engine's config and r its partition */
+/* rank r of nranks; nranks must equal 2^G of the engine's config and r its partition.  Every
+ * answer then ends with ONE ncclAllGather of the partition partials (all queued queries'
+ * nq x efs answers, query-major) + the XOR fold below.  An exchange that fails or does not
+ * enqueue within $PIR_COMM_TIMEOUT seconds (default 60) aborts the communicator; the engine
+ * then refuses every later answer with PIR_ECOMM. */
 int pir_comm_attach(pir_engine_t *e, const uint8_t id[PIR_COMM_ID_BYTES], int nranks, int rank);
+/* the combine step after the all-gather, on its own: d_gathered = nranks blocks of
+ * bytes_per_rank (rank r's partial answers at r * bytes_per_rank: ncclAllGather's output
+ * layout); d_result[i] = XOR over r of d_gathered[r * bytes_per_rank + i] (the XOR assembly of
+ * server.cpp:553-562 across partitions).  Exposed so that one GPU can check a multi-rank
+ * combine against the whole-shard answer before any multi-GPU run. */
+int pir_engine_fold_gathered_dev(pir_engine_t *e, const uint8_t *d_gathered, int nranks,
+                                 uint64_t bytes_per_rank, uint8_t *d_result, void *stream);
 
 #ifdef __cplusplus
 }

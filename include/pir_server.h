@@ -206,6 +206,11 @@ void pirSetDevice(int device);
 /* indexList rows were written by something other than encode_across_files_server: the next
  * query re-uploads the shard to HBM (encode_across_files_server does this implicitly). */
 void pirServerShardChanged(server *s);
+/* Harness helper (no reference counterpart): copy `nrows` packed rows of `rowBytes` bytes
+ * (rowBytes <= the server's fileSizeBytes) into indexList[row0 ..] and mark the shard changed
+ * -- what a test or benchmark would otherwise do row by row through indexList. */
+void pirServerSetRows(server *s, const uint8_t *rows, uint64_t row0, uint64_t nrows,
+                      uint32_t rowBytes);
 
 #ifdef __cplusplus
 }

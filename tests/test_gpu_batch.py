@@ -32,6 +32,9 @@ BATCH_SHAPES = [  # (p, n, efs, nq, num_keys, keys per pass; 0 = automatic)
     (8, 10, 64, 5, 3, 0), (2, 13, 4096, 1, 4, 8), (17, 8, 40, 16, 2, 0), (9, 9, 32, 1, 17, 16),
     # more keys than one frontier launch takes (256): frontiers in several launches
     (2, 6, 16, 1, 300, 0), (3, 7, 24, 2, 270, 4),
+    # 8 share bytes per record and records >= 256 B: k_scan_t over key-major shares (1, 2 and
+    # 4 bytes per key; ragged last groups)
+    (3, 12, 256, 2, 9, 0), (5, 12, 512, 4, 5, 0), (4, 11, 320, 3, 3, 0), (2, 14, 768, 1, 11, 8),
 ]
 
 
@@ -149,3 +152,27 @@ def test_batch_leaf_depth_vs_oracle(pir, monkeypatch, klast, p, n, efs, nq, nk, 
         got = e.answer_batch([k[party] for k in keys])
     for q in range(nk):
         assert np.array_equal(got[q], O.answer(p, party + 1, n, efs, nq, keys[q][party], shard)), q
+
+
+@pytest.mark.parametrize("p,n,efs,nq", [(2, 18, 256, 1), (3, 17, 512, 2), (5, 16, 1024, 4)])
+def test_batch_key_major_equals_interleaved(pir, monkeypatch, p, n, efs, nq):
+    """The key-major share layout with packed 16-byte leaf stores (k_scan_t groups) and the
+    interleaved per-record layout with one store per leaf ($PIR_BATCH_KMAJOR=0,
+    $PIR_LEAF_PACK=0) answer every key of a batch the same; spot keys against the oracle."""
+    rng = np.random.default_rng(n * 13 + p)
+    nk = 19
+    keys = [k[0] for k in _keys(p, n, nq, rng.integers(0, 1 << n, nk), rng)]
+    out = {}
+    for mode, env in (("kmaj", {}), ("inter", {"PIR_BATCH_KMAJOR": "0", "PIR_LEAF_PACK": "0"})):
+        for k in ("PIR_BATCH_KMAJOR", "PIR_LEAF_PACK"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with pir.Engine(p, 1, n, efs, nq) as e:
+            e.fill_shard_random(0x4B4D)
+            out[mode] = e.answer_batch(keys)
+            if mode == "kmaj":
+                shard = e.get_shard()
+    assert np.array_equal(out["kmaj"], out["inter"])
+    for q in (0, nk - 1):
+        assert np.array_equal(out["kmaj"][q], O.answer(p, 1, n, efs, nq, keys[q], shard.reshape(-1))), q

@@ -7,11 +7,15 @@
   configs[4]  2^24 x 1 KiB, p=8, NR=5  per-round share property over several parties; the
                                        encoded shards of all 8 servers, 2 dropped, decode
 
-The oracle cannot answer these sizes in a test's time, so the checks are the reference's own
-answers where it finishes here (golden), else size-independent properties of the protocol:
-ans_0 ^ ans_j == finalCW[r][j] * record (dpf_tree.cpp:142-274 key structure), XOR of
-partition answers == whole answer (linearity over rows), and erasure decode == the record
-(client.cpp:211-268).  One resident shard serves every party via pir_engine_set_party_index.
+The oracle cannot answer these sizes in a test's time.  Where the reference itself finished
+here, the check is its own answers byte for byte: configs[1] (fullsize.json), and at 2^24 rows
+north_star p=2, configs[4] p=8 NR=5 (parties 0/1/7) and configs[2] 256 B x 4 keys
+(fullsize24.json, libref over the engine's device shard generator).  The other keys and shapes
+(128 batched keys, the 2^27 engine, the encode/drop/decode pipeline) are checked through
+size-independent properties of the protocol: ans_0 ^ ans_j == finalCW[r][j] * record
+(dpf_tree.cpp:142-274 key structure), XOR of partition answers == whole answer (linearity over
+rows), and erasure decode == the record (client.cpp:211-268).  One resident shard serves every
+party via pir_engine_set_party_index.
 """
 import numpy as np
 import pytest
@@ -184,13 +188,26 @@ def test_c4_single_engine_and_partitions(pir):
         rec = e.shard_row(idxs[0])
     assert np.array_equal(full[0][0] ^ other[0], _gf_table(int(fcw[0]))[rec])
     acc = np.zeros_like(full)
+    parts = []
     for part in range(1 << G):
         with pir.Engine(p, 1, n, efs, nq, log_num_partitions=G, partition_index=part) as e:
             e.fill_shard_random(0xC4)
-            acc ^= e.answer_stream([k[0] for k in keys])
+            parts.append(e.answer_stream([k[0] for k in keys]))
+            acc ^= parts[-1]
             if part == 0:
                 single0 = e.answer(keys[0][0])
+            if part == (1 << G) - 1:
+                # the split-shard combine of the 8-rank layout (pir_engine.cpp exchange():
+                # ncclAllGather of each rank's K x nq x efs queue partials, rank-major, then the
+                # XOR fold) fed the 8 real partition answers: equals the 128 GiB engine's queue
+                per_rank = full.nbytes
+                d_g = e.alloc_dev(per_rank * len(parts))
+                d_r = e.alloc_dev(per_rank)
+                e.h2d(d_g, np.concatenate([q.reshape(-1) for q in parts]))
+                e.fold_gathered_dev(d_g, len(parts), per_rank, d_r)
+                folded = e.d2h(d_r, per_rank).reshape(full.shape)
     assert np.array_equal(acc, full)
+    assert np.array_equal(folded, full)
     assert single0.any()
 
 

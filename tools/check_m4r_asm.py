@@ -7,9 +7,11 @@ s_bfe_u32 index extracts, and v_xor_b32 whose src0 (the indexed operand) is a co
 register (v96-v127).  Every index change is followed directly by an s_nop or an s_bfe_u32 (the
 stale-index hazard, tools/micro/scan_m4r.hip).  In the functions that fold, no SGPR
 spill lane (v_writelane_b32) lands in the combination registers.  The windows leave M0 holding
-the index (s_set_gpr_idx_off does not restore it; the folds declare "m0" clobbered): after a
-window, no instruction may read M0 before something writes it again (linear order; loops are
-covered by the clobber, which makes the compiler re-materialise M0 where it needs it).
+the index (s_set_gpr_idx_off does not restore it), so every fold tools/gen_m4r.py emits saves
+M0 into an SGPR before its first window and restores it after its last: the compiler's M0
+survives the fold, across loop back-edges too.  The linear-order check below (after a window,
+no instruction reads M0 before something writes it again -- the restore is such a write) is a
+backstop that catches a fold emitted without the save/restore.
 
     python tools/check_m4r_asm.py [lib]
 """

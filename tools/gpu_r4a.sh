@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 4, first GPU pass: thread-call shape + key-major batch parity, then the driver bench and
+# a same-box A/B of the configs[2] batched leg (key-major packed shares vs interleaved)
+set -o pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/test_gpu_threads.py tests/test_gpu_batch.py -x -v \
+  --timeout 200 --timeout-method thread > gpurun_out/r4a_pytest.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --config c3b --steps 3 --warmup 1 > gpurun_out/r4a_c3b_new.json 2>&1 || exit $?
+PIR_BATCH_KMAJOR=0 PIR_LEAF_PACK=0 timeout -k 10 300 python -u bench.py --config c3b --steps 3 --warmup 1 \
+  > gpurun_out/r4a_c3b_old.json 2>&1 || exit $?
+timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r4a_bench.json 2> gpurun_out/r4a_bench.err
