@@ -352,20 +352,25 @@ def measure(ctx, eng, keys, W, K, single=True):
     return out
 
 
-def pir_check(ctx, eng, keyset, fcw, q_answers, n, g):
-    """Full-size PIR property on every rank: the party-1 answers (from the queue) XOR the
-    party-2 answers of the same queries == finalCW * record (p = 2, one round)."""
+def pir_check(ctx, eng, keyset, fcw, q_answers, n, g, parties=(2,)):
+    """Full-size PIR property on every rank: for each party j (1-based) in `parties`, round r of
+    the party-1 answers (from the queue) XOR round r of party j's answers of the same queries ==
+    finalCW[r][j] * record (the key structure of dpf_tree.cpp:142-274; finalCW[r][j] at
+    fcw[r * (p - 1) + j - 2], client.cpp:144-153)."""
     import erasurecodedpir_amd as pir  # noqa: F401
-    tab = _gf_table(int(fcw[0]))
-    eng.set_party(2)
+    nq, p1 = eng.num_rounds, len(keyset[0][1]) - 1
     ok = True
-    for q, (idx, ks) in enumerate(keyset):
-        a2 = ctx.fold(eng.answer(ks[1]))
-        owner = idx >> (n - g) if g else 0
-        rec = eng.shard_row(idx - owner * eng.num_rows) if ctx.rank == owner else None
-        if ctx.world > 1:
-            rec = broadcast_from(rec, owner, eng.record_bytes)
-        ok &= bool(np.array_equal(q_answers[q][0] ^ a2[0], tab[rec]))
+    for j in parties:
+        eng.set_party(j)
+        for q, (idx, ks) in enumerate(keyset):
+            aj = ctx.fold(eng.answer(ks[j - 1]))
+            owner = idx >> (n - g) if g else 0
+            rec = eng.shard_row(idx - owner * eng.num_rows) if ctx.rank == owner else None
+            if ctx.world > 1:
+                rec = broadcast_from(rec, owner, eng.record_bytes)
+            for r in range(nq):
+                tab = _gf_table(int(fcw[r * p1 + j - 2]))
+                ok &= bool(np.array_equal(q_answers[q][r] ^ aj[r], tab[rec]))
     eng.set_party(1)
     return ok
 
@@ -395,6 +400,20 @@ VALU_PEAK_SPEC_T = 256 * 128 * 2.4e9 / 1e12  # lane-ops/s: 256 CUs x 4 SIMD-32 x
 VALU_PEAK_MEASURED_T = 47.0  # 2-VGPR-source bitwise ops, all CUs (profiles/r02_micro/valu_rate.log)
 
 
+def _lib_sha256():
+    import hashlib
+    h = hashlib.sha256()
+    with open(os.path.join(ROOT, "erasurecodedpir_amd", "libpir_engine.so"), "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def _pmc_current(d):
+    """A committed counter summary describes the loaded library only if it carries its sha."""
+    return d.get("lib_sha256") is not None and d.get("lib_sha256") == _lib_sha256()
+
+
 def _valu_roofline(config, world, kern_ms, queries_per_launch, leaves_per_query):
     """Integer-VALU ceiling of the dominant kernel (the AES tree's secondary
     roofline): VALU lane-ops per launch from the committed rocprofv3 --pmc SQ_INSTS_VALU pass
@@ -404,6 +423,8 @@ def _valu_roofline(config, world, kern_ms, queries_per_launch, leaves_per_query)
         return None
     try:
         d = json.load(open(path))
+        if not _pmc_current(d):  # counters of another build: not quoted
+            return None
         c = d.get("counters_per_launch", {})
         insts = c.get("SQ_INSTS_VALU")
         if not insts:
@@ -431,10 +452,15 @@ def _pmc_traffic(config, world, queries_per_launch):
     if world != 1 or not os.path.exists(path):
         return None, None
     try:
-        per_q = json.load(open(path)).get("hbm_bytes_per_query")
-        return (int(per_q * queries_per_launch) if per_q else None,
-                f"profiles/pmc_{config}.json (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, gfx950 "
-                f"corrections), bytes per query x {queries_per_launch}")
+        d = json.load(open(path))
+        per_q = d.get("hbm_bytes_per_query")
+        if not per_q:
+            return None, None
+        src = (f"profiles/pmc_{config}.json (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, gfx950 "
+               f"corrections), bytes per query x {queries_per_launch}")
+        if not _pmc_current(d):
+            src = "stale: " + src + " -- taken from a different libpir_engine.so build"
+        return int(per_q * queries_per_launch), src
     except (OSError, ValueError):
         return None, None
 
@@ -530,7 +556,8 @@ def main():
     timed = keyset[W:]
     # PIR correctness at full size on every rank (the party-2 answers come from the same
     # resident shard, answered as party 2)
-    pir_ok = pir_check(ctx, eng, timed[:4], fcw, m["answers"], n, g) if (p == 2 and nq == 1) else None
+    pir_ok = pir_check(ctx, eng, timed[:4] if p == 2 else timed[:2], fcw, m["answers"], n, g,
+                       parties=sorted({2, p}))
     # host API (key H2D + answer D2H + sync): the PCIe-inclusive rate
     k0 = timed[0][1][0]
     incl_steps = min(20, K)
@@ -701,7 +728,12 @@ def extra_leg(ctx, pir, config, W, K, rng, single=True):
     eng = pir.Engine(p, 1, n, efs, nq, device=ctx.local)
     eng.fill_shard_random(SHARD_SEED)
     m = measure(ctx, eng, [ks[0] for _, ks in keyset], W, K, single=single)
-    ok = pir_check(ctx, eng, keyset[W:W + 2], fcw, m["answers"], n, 0) if (p == 2 and nq == 1) else None
+    # every round's share property against parties 2 and p (all of them for p = 2)
+    ok = pir_check(ctx, eng, keyset[W:W + 2], fcw, m["answers"], n, 0,
+                   parties=sorted({2, p}))
+    # queue == one launch per query (the first two timed keys, when the leg times no singles)
+    q1 = None if single else all(np.array_equal(eng.answer(keyset[W + i][1][0]), m["answers"][i])
+                                 for i in range(min(2, K)))
     eng.close()
     gib = float(1 << n) * efs / GIB
     kern = m["phases"].get("scan", float("nan"))
@@ -715,6 +747,8 @@ def extra_leg(ctx, pir, config, W, K, rng, single=True):
                                "value": round(gib / (m["ms1"] / 1e3), 3), "unit": "GiB/s",
                                "note": "batch = 1: one launch per query"}
         res["queue_equals_one_at_a_time"] = bool(np.array_equal(m["answers"], m["singles"]))
+    else:
+        res["queue_equals_one_at_a_time"] = bool(q1)
     return res
 
 

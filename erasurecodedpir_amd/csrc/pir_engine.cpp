@@ -144,7 +144,6 @@ struct pir_engine {
   // launch); 2 = every workgroup adds its partial to the answer with memory-side atomics
   // (answers of efs % 4 == 0 bytes at 4-byte aligned addresses; else k_reduce)
   int fused_reduce = 0;
-  uint32_t red_gen = 0;  // mode 2: non-zero selects the atomic reduce in k_query
   uint8_t* d_coef_stage = nullptr;  // explicit-coefficient answers: host vectors staged here
   size_t coef_stage_cap = 0;
   uint8_t* d_mpkey = nullptr;       // multiparty DPF keys: host keys / unaligned device keys
@@ -316,18 +315,16 @@ int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, 
   const pir::ScanShape& sh = qp.shape;
   int rc = ensure_slabs(e, (size_t)nk * pir::query_slab_bytes(qp));
   if (!rc) rc = ensure_buf(&e->d_qscratch, &e->qscratch_cap, pir::query_scratch_bytes(qp));
-  // mode 2 needs whole answer words at aligned addresses; otherwise k_reduce (always for slices)
-  const int fred = nslices > 1 || (e->fused_reduce == 2 && (c.record_bytes % 4 != 0 ||
-                                            reinterpret_cast<uintptr_t>(d_out) % 4 != 0))
-                       ? 0 : e->fused_reduce;
-  if (!rc && fred) rc = ensure_qcnt(e, nk, s);
+  // modes 2 and 3 need whole answer words at aligned addresses, mode 3 at least 8 slabs;
+  // otherwise k_reduce (always for slices)
+  int fred = e->fused_reduce;
+  if (fred >= 2 && (c.record_bytes % 4 != 0 || reinterpret_cast<uintptr_t>(d_out) % 4 != 0)) fred = 0;
+  if (fred == 3 && qp.lr < 3) fred = 1;
+  if (nslices > 1) fred = 0;
+  if (!rc && fred) rc = ensure_qcnt(e, nk * (fred == 3 ? 8 : 1), s);
   if (rc) return rc;
-  uint32_t gen = 0;
-  if (fred == 2) {  // the workgroups XOR into zeroed answers
-    if (++e->red_gen == 0) ++e->red_gen;
-    gen = e->red_gen;
+  if (fred >= 2)  // the workgroups (mode 2) or slab groups (mode 3) XOR into zeroed answers
     HIP_TRY(hipMemsetAsync(d_out, 0, (size_t)nk * c.num_rounds * c.record_bytes, s));
-  }
   e->last_chunks = 1;
   e->last_fused = 2;
   hipEvent_t* ev = e->ev;
@@ -341,7 +338,7 @@ int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, 
   HIP_TRY(pir::launch_query(qp, d_raw, (uint32_t)e->key_len, nk, c.num_parties,
                             c.log_num_records, c.party_index - 1, log_parts_total, prefix,
                             e->d_shard + row0 * e->pitch, e->d_slabs, e->d_qscratch, s, nullptr,
-                            fred ? d_out : nullptr, e->d_qcnt, c.record_bytes, gen));
+                            fred ? d_out : nullptr, e->d_qcnt, c.record_bytes, (uint32_t)fred));
   if (ev) {
     HIP_TRY(hipEventRecord(ev[EV_SCAN_E], s));
     HIP_TRY(hipEventRecord(ev[EV_PRERED], s));
@@ -875,7 +872,7 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
     const char* qy = getenv("PIR_QUERY");
     e->allow_query = !(qy && qy[0] == '0');
     const char* fr = getenv("PIR_FUSED_REDUCE");
-    if (fr) e->fused_reduce = std::max(0, std::min(2, atoi(fr)));
+    if (fr) e->fused_reduce = std::max(0, std::min(3, atoi(fr)));
     const char* bg = getenv("PIR_BATCH_G");
     if (bg) e->batch_group = atoi(bg);
     const char* bb = getenv("PIR_BATCH_SCAN_BPC");
@@ -1114,7 +1111,7 @@ int pir_engine_reserve_queue(pir_engine_t* e, int num_keys) {
   if (!qp.tile) return PIR_OK;  // shapes k_query does not take allocate per answer
   int rc = ensure_slabs(e, (size_t)num_keys * pir::query_slab_bytes(qp));
   if (!rc) rc = ensure_buf(&e->d_qscratch, &e->qscratch_cap, pir::query_scratch_bytes(qp));
-  if (!rc && e->fused_reduce) rc = ensure_qcnt(e, num_keys, e->stream);
+  if (!rc && e->fused_reduce) rc = ensure_qcnt(e, num_keys * 8, e->stream);
   if (!rc && e->comm) {
     const size_t total = (size_t)num_keys * c.num_rounds * c.record_bytes;
     rc = ensure_buf(&e->d_bpart, &e->bpart_cap, total);

@@ -178,14 +178,15 @@ constexpr int kQueryTraceSlots = 192;  // trace: per-workgroup phase stamps (wal
 // device scratch for the super-tile tile inputs (0 when ls == 0)
 size_t query_scratch_bytes(const QueryPlan& qp);
 // out != nullptr: the answers are reduced in-kernel (no launch_reduce): query k's nq x efs bytes
-// at out + k * nq * efs.  gen == 0: qcnt = nk zeroed counters (the kernel leaves them zero),
-// the last workgroup reduces; gen != 0: every workgroup adds its partial with memory-side
-// atomics into answers the host zeroed before the launch (efs % 4 == 0)
+// at out + k * nq * efs, by red_mode (k_query): 1 = the last workgroup reduces every slab (qcnt
+// = nk zeroed counters, left zero); 2 = every workgroup adds its partial with memory-side
+// atomics; 3 = the last workgroup of each of 8 slab groups adds the group's XOR (qcnt = 8 nk
+// counters).  Modes 2-3: answers the host zeroed before the launch, efs % 4 == 0.
 hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
                         int p, int n, int party0, int log_parts, uint64_t prefix,
                         const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
                         uint64_t* trace = nullptr, uint8_t* out = nullptr,
-                        uint32_t* qcnt = nullptr, uint32_t efs = 0, uint32_t gen = 0);
+                        uint32_t* qcnt = nullptr, uint32_t efs = 0, uint32_t red_mode = 0);
 // XOR the slabs, compact pitch -> record_bytes: d_out[a*efs + b]; nk queries (slabs of query k
 // grid.x*grid.y*slab_bytes apart, answers nq*efs bytes apart).  nslices > 1 (dividing grid.x):
 // per query, nslices answers over consecutive equal runs of the grid.x slabs, i.e. over equal

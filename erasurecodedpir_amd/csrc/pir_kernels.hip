@@ -1234,13 +1234,15 @@ __global__ __launch_bounds__(NT) void k_query(
     uint4* __restrict__ fr_s, uint32_t* __restrict__ fr_t, const uint8_t* __restrict__ shard,
     uint32_t pitch, uint32_t cpr, uint32_t gy, uint8_t* __restrict__ slabs,
     uint64_t* __restrict__ trace, uint8_t* __restrict__ out, uint32_t* __restrict__ qcnt,
-    uint32_t efs, uint32_t red_gen) {
+    uint32_t efs, uint32_t red_mode) {
   // out != nullptr: the slabs of each query are reduced in-kernel into out (query k at
-  // out + k * nq * efs); else the host launches k_reduce.  red_gen == 0: the last workgroup to add
-  // to qcnt[k] (zero on entry, left zero) XORs every slab.  red_gen != 0 (efs % 4 == 0, out 4-byte
-  // aligned): every workgroup XORs its partial answer into out with memory-side atomics; the
-  // host zeroes out (hipMemsetAsync on the launch's stream) before the launch -- no slab
-  // traffic and no single-workgroup tail.
+  // out + k * nq * efs); else the host launches k_reduce.  red_mode 1: the last workgroup to
+  // add to qcnt[k] (zero on entry, left zero) XORs every slab.  Modes 2 and 3 (efs % 4 == 0,
+  // out 4-byte aligned) XOR into answers the host zeroed (hipMemsetAsync on the launch's
+  // stream) with memory-side atomics: 2 = every workgroup its own partial (no slab traffic, no
+  // single-workgroup tail); 3 = per group of the workgroups b = x mod 8 (one XCD each under
+  // round-robin dispatch), the last of the group to add to qcnt[8k + x] XORs the group's slabs
+  // and adds that ONE partial (8 atomic adds per answer word instead of 2^lr).
   // trace != nullptr: per-workgroup wall-clock stamps (100 MHz) of query 0's phases,
   // kQueryTraceSlots apart (layout: pir_engine_trace_query, include/pir_engine.h)
   // diagnostics only: trace[kQueryTraceSlots * gridDim.x] bit 0 = scan waves skip their rows
@@ -1267,7 +1269,8 @@ __global__ __launch_bounds__(NT) void k_query(
   }
   // atomic_red: the answers were zeroed by a memset the host enqueued before this launch (on
   // the same stream), so no workgroup waits on another's progress
-  const bool atomic_red = out && red_gen;
+  const bool atomic_red = out && red_mode == 2;
+  const uint32_t red_groups = red_mode == 3 ? 8u : 1u;  // slab groups of the last-add reduce
   __syncthreads();
   if (trace && threadIdx.x == 0) trace[1] = wall_clock64();
 
@@ -1793,24 +1796,25 @@ __global__ __launch_bounds__(NT) void k_query(
           // release (agent) before the counter add, acquire (agent) in the last workgroup.
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           group_barrier(&sm.sbar, sgen, SW);
+          const uint32_t gx = gridDim.x, xg = (uint32_t)b % red_groups;  // this slab group
+          uint32_t* const cnt = qcnt + (size_t)qy * red_groups + xg;
           if (st == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            sm.lastq = __hip_atomic_fetch_add(qcnt + qy, 1u, __ATOMIC_ACQ_REL,
-                                              __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+            sm.lastq = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL,
+                                              __HIP_MEMORY_SCOPE_AGENT) == gx / red_groups - 1;
           }
           group_barrier(&sm.sbar, sgen, SW);
           if (lds_load(&sm.lastq)) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             const uint32_t words = pitch / 4, P = (uint32_t)NQ * words, nth = SW * 64;
             const uint32_t S = P >= nth ? 1u : nth / P;  // threads per output word
-            const uint32_t gx = gridDim.x;
             for (uint32_t idx = (uint32_t)st; idx < P * S; idx += nth) {
               const uint32_t pw = idx % P, part = idx / P;
               const uint32_t a = pw / words, w = pw - a * words;
               const uint32_t grp = w / GW, win = w - grp * GW;
               const uint32_t* src = qslab + (uint64_t)grp * gx * slab_words + a * GW + win;
               uint32_t acc = 0;
-              for (uint32_t x = part; x < gx; x += S)
+              for (uint32_t x = xg + part * red_groups; x < gx; x += S * red_groups)
                 acc ^= __hip_atomic_load(src + (uint64_t)x * slab_words, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
               if (acc) atomicXor(&sm.red[grp][a * GW + win], acc);
@@ -1822,11 +1826,15 @@ __global__ __launch_bounds__(NT) void k_query(
               const uint32_t grp = w / GW, win = w - grp * GW;
               const uint32_t v = sm.red[grp][a * GW + win];
               sm.red[grp][a * GW + win] = 0;
-              for (uint32_t t = 0; t < 4; ++t)
-                if (4 * w + t < efs) qout[(size_t)a * efs + 4 * w + t] = (uint8_t)(v >> (8 * t));
+              if (red_groups > 1) {  // one of the groups' partials: add it to the zeroed answer
+                if (v && 4 * w < efs) atomicXor(reinterpret_cast<uint32_t*>(qout + (size_t)a * efs) + w, v);
+              } else {
+                for (uint32_t t = 0; t < 4; ++t)
+                  if (4 * w + t < efs) qout[(size_t)a * efs + 4 * w + t] = (uint8_t)(v >> (8 * t));
+              }
             }
             if (st == 0)  // ready for the next launch that answers a query in this slot
-              __hip_atomic_store(qcnt + qy, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         }
         group_barrier(&sm.sbar, sgen, SW);  // red[] is clear for the next query
@@ -2208,7 +2216,7 @@ static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t k
                            int p, int n, int party0, int log_parts, uint64_t prefix,
                            const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
                            uint64_t* trace, uint8_t* out, uint32_t* qcnt, uint32_t efs,
-                           uint32_t gen) {
+                           uint32_t red_mode) {
   uint4* fr_s = reinterpret_cast<uint4*>(scratch);
   uint32_t* fr_t = reinterpret_cast<uint32_t*>(scratch + ((size_t)qp.shape.grid.x << (kQueryKin + qp.ls)) * sizeof(uint4));
   constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : 8));
@@ -2219,7 +2227,7 @@ static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t k
   hipLaunchKernelGGL((k_query<NQ, NRP, VEC, UNI, TW, TILE, GY, RING, NTH>), dim3(sh.grid.x),     \
                      dim3(NTH), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,                    \
                      log_parts, prefix, qp.lr, qp.lt, qp.ls, fr_s, fr_t, shard, sh.pitch, sh.cpr,  \
-                     gy, slabs, trace, out, qcnt, efs, gen)
+                     gy, slabs, trace, out, qcnt, efs, red_mode)
 #define PIR_QL(UNI, TW, GY, gy) PIR_QLN(UNI, TW, GY, gy, kFusedThreads)
   if constexpr (VEC == 2 && NQ >= 4 && NQ <= 5 && NQ > PIR_QUERY_BRANCH_MAXNQ && TILE == 1024) {
     if (sh.uniform && qp.m4r) {  // four-Russians scan waves (k_query's kM4R)
@@ -2250,11 +2258,12 @@ hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_
                         int p, int n, int party0, int log_parts, uint64_t prefix,
                         const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
                         uint64_t* trace, uint8_t* out, uint32_t* qcnt, uint32_t efs,
-                        uint32_t gen) {
+                        uint32_t red_mode) {
   if (nk < 1 || (qp.ls && !scratch) || (out && !qcnt)) return hipErrorInvalidValue;
-  if (out && gen && (efs % 4 != 0 || reinterpret_cast<uintptr_t>(out) % 4 != 0))
+  if (out && (red_mode < 1 || red_mode > 3 || (qp.lr < 3 && red_mode == 3))) return hipErrorInvalidValue;
+  if (out && red_mode >= 2 && (efs % 4 != 0 || reinterpret_cast<uintptr_t>(out) % 4 != 0))
     return hipErrorInvalidValue;
-#define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, scratch, s, trace, out, qcnt, efs, gen)
+#define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, scratch, s, trace, out, qcnt, efs, red_mode)
 #ifdef PIR_DEV_NQ  // development builds only (ISA / register checks): one round count
   return qp.shape.nq == PIR_DEV_NQ && qp.tile == 1024 ? PIR_Q(PIR_DEV_NQ, 1024) : hipErrorInvalidValue;
 #else

@@ -24,6 +24,8 @@ fi
 BENCH="python bench.py --steps $K --warmup $K --no-cpu --queue-only"
 for cfg in ${CONFIGS:-c24}; do
   rm -rf gpurun_out/prof_$cfg
+  # the library these counters describe (bench.py flags a summary whose sha differs as stale)
+  sha256sum erasurecodedpir_amd/libpir_engine.so > gpurun_out/pmc_${cfg}_lib_sha256.txt
   run trace_$cfg 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$cfg -o run --output-format csv -- $BENCH --config $cfg
   for pass in ${PASSES:-traffic insts}; do
     case $pass in

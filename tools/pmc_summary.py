@@ -43,6 +43,15 @@ def issue_block(avg, avg_ns, algo):
         d["valu_insts_per_shard_dword"] = round(avg["SQ_INSTS_VALU"] * 64 / (algo / 4), 3)
     if "SQ_INSTS_SALU" in avg:
         d["salu_insts_per_shard_dword"] = round(avg["SQ_INSTS_SALU"] * 64 / (algo / 4), 3)
+    # where the waves' cycles go (SQ_WAVE_CYCLES = ACTIVE_INST_ANY + WAIT_INST_ANY + WAIT_ANY,
+    # disjoint; all quad-cycle counters, so the shares need no unit)
+    if "SQ_WAVE_CYCLES" in avg:
+        wc = avg["SQ_WAVE_CYCLES"]
+        for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_VALU",
+                  "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_MISC",
+                  "SQ_INST_CYCLES_SALU"):
+            if k in avg:
+                d["share_of_wave_cycles_" + k[3:].lower()] = round(avg[k] / wc, 4)
     return d
 
 
@@ -90,7 +99,10 @@ def main():
     avg = {k: sum(v) / len(v) for k, v in counters.items()}
     nl = {k: len(v) for k, v in counters.items()}
     algo = nrec * efs * qpl
+    sha_f = os.path.join(base, f"pmc_{cfg}_lib_sha256.txt")  # written by tools/gpu_pmc.sh
+    lib_sha = open(sha_f).read().split()[0] if os.path.exists(sha_f) else None
     out = {"config": cfg, "kernel": name.split("(")[0], "queries_per_launch": qpl,
+           "lib_sha256": lib_sha,
            "kernel_avg_ns_rocprof": avg_ns, "achieved_GBps_rocprof": round(algo / avg_ns, 1),
            "algorithmic_bytes_per_launch": algo,
            "counters_per_launch": {k: round(v, 1) for k, v in sorted(avg.items())},
