@@ -204,12 +204,9 @@ void k_scan_t(const uint8_t* __restrict__ shard, uint64_t nrec, uint32_t pitch, 
 }
 
 // $PIR_SCAN_T: 0 = never, 2 = every 4-8 round shape it can take (diagnostics), else the default
-static int scan_t_mode() {
-  static const int mode = [] {
-    const char* v = getenv("PIR_SCAN_T");
-    return v ? atoi(v) : 1;
-  }();
-  return mode;
+static int scan_t_mode() {  // read per plan (tests switch it within one process)
+  const char* v = getenv("PIR_SCAN_T");
+  return v ? atoi(v) : 1;
 }
 bool scan_t_enabled() { return scan_t_mode() != 0; }
 
