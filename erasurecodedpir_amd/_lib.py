@@ -190,6 +190,8 @@ PROTOTYPES = {
     "assembleWoodruffResponses": (None, [ctypes.POINTER(CClient), _P, _P, _P, _P]),
     "pirSetDevice": (None, [_I]),
     "pirServerShardChanged": (None, [ctypes.POINTER(CServer)]),
+    "pirRunTreeQueryThreads": (None, [ctypes.POINTER(CServer), ctypes.c_void_p, ctypes.c_int,
+                                      ctypes.c_void_p]),
     "pirServerSetRows": (None, [ctypes.POINTER(CServer), ctypes.c_void_p, ctypes.c_uint64,
                                 ctypes.c_uint64, ctypes.c_uint32]),
 }

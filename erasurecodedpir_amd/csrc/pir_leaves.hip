@@ -55,6 +55,48 @@ __device__ __forceinline__ uint4 leaf_value4(const Tab4& T, const DevKey* __rest
   return o[0];
 }
 
+// The AES flavour of a subtree walk: the 4-table T-box (pir_aes4.h, 128 KiB of LDS: one
+// 1024-thread workgroup per CU) or, T2, the 2-table T-box of pir_aes.h (64 KiB: two workgroups
+// per CU, so kLeaf2Threads x 2 threads at amdgpu_waves_per_eu(kLeaf2WPE) -- more waves in
+// flight for an LDS-latency-bound walk at the price of 2 v_alignbit per column).
+template <bool T2> struct AesF;
+template <> struct AesF<false> {
+  using TabT = Tab4;
+  template <int TB>
+  __device__ __forceinline__ static void node(const Tab4& T, const DevKey* __restrict__ K, int L,
+                                              const Bits& B, uint4 s, uint32_t t, uint4& sl,
+                                              uint4& sr, uint32_t& tl, uint32_t& tr) {
+    expand_node4<TB>(T, K, L, B, s, t, sl, sr, tl, tr);
+  }
+  template <int NRP>
+  __device__ __forceinline__ static uint4 leaf(const Tab4& T, const DevKey* __restrict__ K,
+                                               uint32_t pm1, uint4 s, uint32_t t) {
+    return leaf_value4<NRP>(T, K, pm1, s, t);
+  }
+};
+template <> struct AesF<true> {
+  using TabT = Tab;
+  template <int TB>
+  __device__ __forceinline__ static void node(const Tab& T, const DevKey* __restrict__ K, int L,
+                                              const Bits& B, uint4 s, uint32_t t, uint4& sl,
+                                              uint4& sr, uint32_t& tl, uint32_t& tr) {
+    expand_node(T, K, L, B, s, t, sl, sr, tl, tr);
+  }
+  template <int NRP>
+  __device__ __forceinline__ static uint4 leaf(const Tab& T, const DevKey* __restrict__ K,
+                                               uint32_t pm1, uint4 s, uint32_t t) {
+    return leaf_value<NRP <= 4 ? 1 : NRP / 4, (NRP < 4 ? NRP : 0)>(T, K, pm1, s, t);
+  }
+};
+#ifndef PIR_LEAF2_THREADS
+#define PIR_LEAF2_THREADS 768
+#endif
+#ifndef PIR_LEAF2_WPE
+#define PIR_LEAF2_WPE 6
+#endif
+constexpr int kLeaf2Threads = PIR_LEAF2_THREADS;
+constexpr int kLeaf2WPE = PIR_LEAF2_WPE;
+
 // Where a subtree's bottom level goes: the DPF shares of its leaves (leaf stage) or its nodes
 // (seed, control bits) for the next stage (node stage).
 struct DfsOut {
@@ -84,20 +126,21 @@ __device__ __forceinline__ void pack_leaf(uint4& acc, uint32_t v) {
 }
 
 // the 2^D leaves (or bottom nodes) under node (s, t) of level L, indices [i0, i0 + 2^D)
-template <bool NODES, int NRP, int TB, int D, bool PACK>
-__device__ __forceinline__ void subtree_dfs(const Tab4& T, const DevKey* __restrict__ K, int L,
-                                            const Bits& B, uint4 s, uint32_t t, uint64_t i0,
-                                            const DfsOut& o, uint4& acc) {
+template <bool NODES, int NRP, int TB, int D, bool PACK, bool T2>
+__device__ __forceinline__ void subtree_dfs(const typename AesF<T2>::TabT& T,
+                                            const DevKey* __restrict__ K, int L, const Bits& B,
+                                            uint4 s, uint32_t t, uint64_t i0, const DfsOut& o,
+                                            uint4& acc) {
   uint4 sl, sr;
   uint32_t tl, tr;
-  expand_node4<TB>(T, K, L, B, s, t, sl, sr, tl, tr);
+  AesF<T2>::template node<TB>(T, K, L, B, s, t, sl, sr, tl, tr);
   if constexpr (D == 1) {
     if constexpr (NODES) {
       o.s[i0] = sl; o.s[i0 + 1] = sr;
       o.t[i0] = tl; o.t[i0 + 1] = tr;
     } else {
-      const uint4 vl = leaf_value4<NRP>(T, K, B.pm1, sl, tl);
-      const uint4 vr = leaf_value4<NRP>(T, K, B.pm1, sr, tr);
+      const uint4 vl = AesF<T2>::template leaf<NRP>(T, K, B.pm1, sl, tl);
+      const uint4 vr = AesF<T2>::template leaf<NRP>(T, K, B.pm1, sr, tr);
       if constexpr (PACK) {
         constexpr uint32_t LPS = 16 / NRP;  // leaves per 16-byte store
         pack_leaf<NRP>(acc, vl.x & o.qm.x);
@@ -113,15 +156,16 @@ __device__ __forceinline__ void subtree_dfs(const Tab4& T, const DevKey* __restr
     // one copy of the subtree code per level: the right child waits in registers
 #pragma unroll 1
     for (int i = 0; i < 2; ++i)
-      subtree_dfs<NODES, NRP, TB, D - 1, PACK>(T, K, L + 1, B, i ? sr : sl, i ? tr : tl,
-                                               i0 + ((uint64_t)i << (D - 1)), o, acc);
+      subtree_dfs<NODES, NRP, TB, D - 1, PACK, T2>(T, K, L + 1, B, i ? sr : sl, i ? tr : tl,
+                                                   i0 + ((uint64_t)i << (D - 1)), o, acc);
   }
 }
 
 // blockIdx.y = key of a batch: its DevKey, input node range (in_stride apart) and outputs
 // (shares at c + y * c_key_off, or nodes out_stride apart)
-template <bool NODES, int NRP, int TB, int KD, bool PACK = false>
-__global__ __launch_bounds__(kLeafThreads)
+template <bool NODES, int NRP, int TB, int KD, bool PACK = false, bool T2 = false>
+__global__ __launch_bounds__(T2 ? kLeaf2Threads : kLeafThreads)
+__attribute__((amdgpu_waves_per_eu(T2 ? kLeaf2WPE : 4)))
 void k_subtree(const DevKey* __restrict__ K, const uint4* __restrict__ in_s,
                const uint32_t* __restrict__ in_t, int L0, uint64_t nin, uint64_t in_stride,
                uint8_t* __restrict__ c, uint32_t cstride, uint32_t c_key_off,
@@ -129,8 +173,10 @@ void k_subtree(const DevKey* __restrict__ K, const uint4* __restrict__ in_s,
   K += blockIdx.y;
   in_s += blockIdx.y * in_stride;
   in_t += blockIdx.y * in_stride;
-  __shared__ uint32_t tab[kTab4Bytes / 4];
-  load_tables4_n<kLeafThreads>(tab);
+  constexpr int NT = T2 ? kLeaf2Threads : kLeafThreads;
+  __shared__ uint32_t tab[(T2 ? kTablesBytes : kTab4Bytes) / 4];
+  if constexpr (T2) load_tables_n<NT>(tab);
+  else load_tables4_n<NT>(tab);
   const Bits B(K->p);
   DfsOut o;
   if constexpr (NODES) {
@@ -148,11 +194,11 @@ void k_subtree(const DevKey* __restrict__ K, const uint4* __restrict__ in_s,
     o.qm = make_uint4(m[0], m[1], m[2], m[3]);
   }
   __syncthreads();
-  const Tab4 T(tab);
-  const uint64_t u = (uint64_t)blockIdx.x * kLeafThreads + threadIdx.x;
+  const typename AesF<T2>::TabT T(tab);
+  const uint64_t u = (uint64_t)blockIdx.x * NT + threadIdx.x;
   if (u >= nin) return;  // no barrier below
   uint4 acc = make_uint4(0, 0, 0, 0);
-  subtree_dfs<NODES, NRP, TB, KD, PACK>(T, K, L0, B, in_s[u], in_t[u], u << KD, o, acc);
+  subtree_dfs<NODES, NRP, TB, KD, PACK, T2>(T, K, L0, B, in_s[u], in_t[u], u << KD, o, acc);
 }
 
 bool leaves_supported(int kd) { return kd >= kLeavesMinK && kd <= kLeavesMaxK; }
@@ -171,9 +217,11 @@ struct SubtreeArgs {
   uint64_t out_stride;
 };
 
-template <bool NODES, int NRP, int TB, int KD, bool PACK = false>
+template <bool NODES, int NRP, int TB, int KD, bool PACK = false, bool T2 = false>
 static hipError_t subtree_launch(dim3 grid, const SubtreeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((k_subtree<NODES, NRP, TB, KD, PACK>), grid, dim3(kLeafThreads), 0, s,
+  constexpr int NT = T2 ? kLeaf2Threads : kLeafThreads;
+  grid.x = (unsigned)((a.nin + NT - 1) / NT);
+  hipLaunchKernelGGL((k_subtree<NODES, NRP, TB, KD, PACK, T2>), grid, dim3(NT), 0, s,
                      a.key, a.is, a.it, a.L0, a.nin, a.in_stride, a.c, a.cstride, a.c_key_off,
                      a.os, a.ot, a.out_stride);
   return hipGetLastError();
@@ -186,9 +234,19 @@ static hipError_t leaves_kd(int kd, dim3 grid, const SubtreeArgs& a, hipStream_t
   // ($PIR_LEAF_PACK=0: one store per leaf, diagnostics)
   const char* pk = getenv("PIR_LEAF_PACK");
   const bool pack_ok = !(pk && atoi(pk) == 0);
+  // $PIR_LEAF_T2=1 (experiment): the 2-table AES at two workgroups per CU (packed stores only)
+  const char* t2 = getenv("PIR_LEAF_T2");
+  const bool use_t2 = t2 && atoi(t2) == 1;
   if constexpr (NRP <= 4) {
     if (pack_ok && a.cstride == (uint32_t)NRP && (reinterpret_cast<uintptr_t>(a.c) & 15) == 0 &&
         ((uint64_t)a.c_key_off & 15) == 0) {
+      if (use_t2) {
+        switch (kd) {
+          case 4: return subtree_launch<false, NRP, TB, 4, true, true>(grid, a, s);
+          case 5: return subtree_launch<false, NRP, TB, 5, true, true>(grid, a, s);
+          default: return hipErrorInvalidValue;
+        }
+      }
       switch (kd) {
         case 4: return subtree_launch<false, NRP, TB, 4, true>(grid, a, s);
         case 5: return subtree_launch<false, NRP, TB, 5, true>(grid, a, s);

@@ -11,7 +11,12 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
+#include <thread>
 #include <random>
 #include <utility>
 #include <vector>
@@ -135,6 +140,88 @@ pir_engine_t* engine_for(server* s, ShimState* st, int nq) {
     st->dirty = false;
   }
   return st->eng;
+}
+
+// The worker threads of pirRunTreeQueryThreads: created once, T of them per fan-out.  A worker
+// polls (with yields) for ~0.2 ms after each job and then sleeps on the condition variable, so
+// back-to-back queries see goroutine-like wake-ups and an idle process burns no cores.
+class FanoutPool {
+ public:
+  ~FanoutPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      quit_ = true;
+      gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // job(t) for t < n on n pool threads, concurrently; returns when all are done
+  void run(int n, const std::function<void(int)>& job) {
+    std::lock_guard<std::mutex> one(run_mu_);  // one fan-out at a time
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      while ((int)th_.size() < n) {
+        const int i = (int)th_.size();
+        th_.emplace_back([this, i] { worker(i); });
+      }
+      job_ = &job;
+      n_ = n;
+      remaining_.store(n, std::memory_order_relaxed);
+      gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    const auto t0 = std::chrono::steady_clock::now();
+    while (remaining_.load(std::memory_order_acquire) != 0) {
+      if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200)) {
+        std::this_thread::yield();
+      } else {
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return remaining_.load(std::memory_order_acquire) == 0; });
+      }
+    }
+  }
+
+ private:
+  void worker(int i) {
+    uint64_t seen = 0;
+    for (;;) {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (gen_.load(std::memory_order_acquire) == seen &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200))
+        std::this_thread::yield();
+      const std::function<void(int)>* job;
+      int n;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+        seen = gen_.load(std::memory_order_acquire);
+        if (quit_) return;
+        job = job_;
+        n = n_;
+      }
+      if (i < n) {
+        (*job)(i);
+        if (remaining_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+          std::lock_guard<std::mutex> lk(mu_);
+          done_cv_.notify_all();
+        }
+      }
+    }
+  }
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> th_;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<int> remaining_{0};
+  const std::function<void(int)>* job_ = nullptr;
+  int n_ = 0;
+  bool quit_ = false;
+};
+
+FanoutPool& fanout_pool() {
+  static FanoutPool pool;
+  return pool;
 }
 
 int ceil_log2(long v) {
@@ -597,6 +684,30 @@ void runOptimizedDPFTreeQueryThread(server* s, uint8_t* key, int threadNum, int 
   for (int a = 0; a < NUM_ROUNDS; ++a) memcpy(result[a], part + a * efs, efs);
   it->taken[threadNum] = 1;
   if (--it->left == 0) st->groups.erase(it);
+}
+
+// RunTreeQuery's fan-out (src/server_util/tree.go:60-80) for callers without Go: numThreads
+// pool threads call runOptimizedDPFTreeQueryThread(s, key, t, numThreads, .) concurrently (the
+// goroutines), then assemblDPFTreeQueryThreadResults XORs their partials into result.
+void pirRunTreeQueryThreads(server* s, uint8_t* key, int numThreads, uint8_t** result) {
+  if (numThreads < 1) {
+    fprintf(stderr, "pir shim: %d threads\n", numThreads);
+    abort();
+  }
+  const size_t efs = (size_t)ENCODED_FILE_SIZE_BYTES;
+  std::vector<uint8_t> buf((size_t)numThreads * NUM_ROUNDS * efs);
+  std::vector<uint8_t*> rows((size_t)numThreads * NUM_ROUNDS);
+  std::vector<uint8_t**> in((size_t)numThreads);
+  for (int t = 0; t < numThreads; ++t) {
+    for (int a = 0; a < NUM_ROUNDS; ++a)
+      rows[(size_t)t * NUM_ROUNDS + a] = buf.data() + ((size_t)t * NUM_ROUNDS + a) * efs;
+    in[t] = rows.data() + (size_t)t * NUM_ROUNDS;
+  }
+  const std::function<void(int)> job = [&](int t) {
+    runOptimizedDPFTreeQueryThread(s, key, t, numThreads, in[t]);
+  };
+  fanout_pool().run(numThreads, job);
+  assemblDPFTreeQueryThreadResults(s, in.data(), numThreads, result);
 }
 
 // server.cpp:553-562 (host buffers from the Go caller)

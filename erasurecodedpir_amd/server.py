@@ -76,6 +76,17 @@ class Server:
                                                  numThreads, _row_ptrs(out))
         return out
 
+    def runTreeQueryThreads(self, key, numThreads):
+        """RunTreeQuery's fan-out (src/server_util/tree.go:60-80) in the library: numThreads
+        concurrent runOptimizedDPFTreeQueryThread calls + assemblDPFTreeQueryThreadResults."""
+        efs = _lib.global_int("ENCODED_FILE_SIZE_BYTES")
+        nq = _lib.global_int("NUM_ROUNDS")
+        out = np.zeros((nq, efs), np.uint8)
+        k = np.frombuffer(bytes(key), np.uint8).copy()
+        self._lib.pirRunTreeQueryThreads(ctypes.byref(self.s), k.ctypes.data_as(ctypes.c_void_p),
+                                         numThreads, ctypes.cast(_row_ptrs(out), ctypes.c_void_p))
+        return out
+
     def runHollantiQuery(self, keys):
         """keys: (NUM_ROUNDS, NUM_ENCODED_FILES) coefficient vectors (server.cpp:321-343)."""
         return self._hollanti(keys, None)

@@ -201,6 +201,12 @@ void genWoodruffQuery(uint128_t index, int t, int p, int m, uint8_t **v, uint8_t
 void assembleWoodruffResponses(client *c, uint8_t *erasureIndexList, uint8_t ***responses,
                                uint8_t *output, uint8_t **v);
 
+/* Harness helper (the fan-out of src/server_util/tree.go:60-80 for callers without Go):
+ * numThreads threads of a persistent pool call runOptimizedDPFTreeQueryThread(s, key, t,
+ * numThreads, .) concurrently, then assemblDPFTreeQueryThreadResults XORs the partials into
+ * result[round] (ENCODED_FILE_SIZE_BYTES each). */
+void pirRunTreeQueryThreads(server *s, uint8_t *key, int numThreads, uint8_t **result);
+
 /* Engine device used by servers created after this call (default: $PIR_DEVICE or 0). */
 void pirSetDevice(int device);
 /* indexList rows were written by something other than encode_across_files_server: the next
