@@ -1596,6 +1596,7 @@ __global__ __launch_bounds__(NT) void k_query(
     // row slot j of a tile = row group wi + j * nwg; rpt slots per tile, a multiple of U (slots
     // past the tile's row groups are masked)
     const uint32_t rpt = ((ngroups + nwg - 1) / nwg + U - 1) / U * U;
+    constexpr bool kM4RExact = kM4R && SW == 8 && TILE == 1024 && 128 % U == 0;
     const bool scan = wi < nwg && !(trace && trace_flags_noscan);
     __builtin_amdgcn_s_setprio(PIR_SCAN_PRIO);
     const uint8_t* rbase = shard + (b * region_rows) * pitch + (uint64_t)chunk * CH;
@@ -1620,7 +1621,9 @@ __global__ __launch_bounds__(NT) void k_query(
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(rgn + (uint64_t)(g & (ntiles - 1)) * tile_bytes), (short)0,
             g < total ? (int)tile_bytes : 0, kBufRsrcWord3);
-        dst = load_chunk_buf<VEC>(rs, lane_off, gi < ngroups ? gi * pitch : 0u);
+        // four-Russians scan waves at 8 per workgroup: nwg = 8 / gy divides 8, so with TILE =
+        // 1024 rows and U | 128 every slot holds a row -- no guard, two SALU fewer per row
+        dst = load_chunk_buf<VEC>(rs, lane_off, (kM4RExact || gi < ngroups) ? gi * pitch : 0u);
       } else {
         const uint32_t rl = gi * rpw + rec_off;
         const bool ok = g < total && active && gi < ngroups && rl < TILE;

@@ -15,7 +15,9 @@
 #include <chrono>
 #include <condition_variable>
 #include <functional>
+#include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <thread>
 #include <random>
 #include <utility>
@@ -74,24 +76,34 @@ int device_default() {
 // that tree.go:60-76 issues with the same key: the first call to arrive answers every slice in
 // one engine pass (pir_engine_answer_slices), the others copy theirs out.  An entry lives
 // until each of its T slices has been taken once (or the shard / engine changes).
+// The computing call publishes `state` (1 = parts ready, -1 = the engine failed); the other
+// calls of the group wait for it WITHOUT the server lock -- polling with yields for a few ms (a
+// query's pass), then sleeping on `cv` -- so the T - 1 waiters copy their slices concurrently
+// instead of queueing for the server lock one by one.
 struct SliceGroup {
   std::vector<uint8_t> key;
   int num_threads = 0;
-  std::vector<uint8_t> parts;   // num_threads x NUM_ROUNDS x efs
-  std::vector<uint8_t> taken;   // per slice
-  int left = 0;
+  std::vector<uint8_t> parts;     // num_threads x NUM_ROUNDS x efs (immutable once published)
+  std::vector<uint8_t> taken;     // per slice, under ShimState::mu
+  std::atomic<int> left{0};       // slices not yet copied out
+  std::atomic<int> state{0};
+  std::mutex m;
+  std::condition_variable cv;
 };
 constexpr size_t kMaxSliceGroups = 8;  // queries whose slices are in flight at once
 
 // Per-server engine state, hung off server.ctx.
 struct ShimState {
   std::mutex mu;
+  // held shared by a slice group's engine pass (which runs without mu); engine_for takes it
+  // exclusively (under mu) before it replaces the engine or re-uploads the shard
+  std::shared_mutex life;
   pir_engine_t* eng = nullptr;
   pir_engine_config cfg{};
   bool dirty = true;  // indexList changed since the last upload
   uint32_t rows_alloc = 0;
   uint32_t row_bytes = 0;          // bytes per indexList row (initializeServer's fileSizeBytes)
-  std::vector<SliceGroup> groups;  // oldest first
+  std::vector<std::shared_ptr<SliceGroup>> groups;  // oldest first
 };
 
 ShimState* state_of(server* s) {
@@ -120,8 +132,13 @@ pir_engine_t* engine_for(server* s, ShimState* st, int nq) {
   c.log_num_partitions = 0;
   c.partition_index = 0;
   c.is_byzantine = s->isByzantine;
-  if (!st->eng || memcmp(&c, &st->cfg, sizeof c) != 0 || st->dirty) st->groups.clear();
-  if (!st->eng || memcmp(&c, &st->cfg, sizeof c) != 0) {
+  const bool remake = !st->eng || memcmp(&c, &st->cfg, sizeof c) != 0;
+  std::unique_lock<std::shared_mutex> excl(st->life, std::defer_lock);
+  if (remake || st->dirty) {  // no slice pass may be using the engine or the shard meanwhile
+    excl.lock();
+    st->groups.clear();
+  }
+  if (remake) {
     if (st->eng) pir_engine_destroy(st->eng);
     st->eng = nullptr;
     if (pir_engine_create(&c, &st->eng) != PIR_OK) die("pir_engine_create");
@@ -652,38 +669,68 @@ void runOptimizedDPFTreeQuery(server* s, uint8_t* key, int numQueries, uint8_t**
 void runOptimizedDPFTreeQueryThread(server* s, uint8_t* key, int threadNum, int numThreads,
                                     uint8_t** result) {
   ShimState* st = state_of(s);
-  std::lock_guard<std::mutex> lk(st->mu);
-  pir_engine_t* e = engine_for(s, st, NUM_ROUNDS);
-  if (!key || numThreads < 1 || threadNum < 0 || threadNum >= numThreads ||
-      (numThreads & (numThreads - 1)) || numThreads > NUM_ENCODED_FILES) {
-    fprintf(stderr, "pir shim: thread %d of %d (a power of two <= %d rows)\n", threadNum,
-            numThreads, NUM_ENCODED_FILES);
-    abort();
-  }
+  std::shared_ptr<SliceGroup> g;
+  pir_engine_t* e = nullptr;
+  std::shared_lock<std::shared_mutex> pass;  // the computing call's hold on the engine
   const size_t efs = (size_t)ENCODED_FILE_SIZE_BYTES, ans = (size_t)NUM_ROUNDS * efs;
-  const size_t klen = (size_t)calcOptimizedDPFTreeKeyLength(NUM_PARTIES < 2 ? 2 : NUM_PARTIES,
-                                                            LOG_NUM_ENCODED_FILES, NUM_ROUNDS);
-  auto it = std::find_if(st->groups.begin(), st->groups.end(), [&](const SliceGroup& g) {
-    return g.num_threads == numThreads && !g.taken[threadNum] &&
-           memcmp(g.key.data(), key, klen) == 0;
-  });
-  if (it == st->groups.end()) {
-    if (st->groups.size() >= kMaxSliceGroups) st->groups.erase(st->groups.begin());
-    SliceGroup g;
-    g.key.assign(key, key + klen);
-    g.num_threads = numThreads;
-    g.parts.resize((size_t)numThreads * ans);
-    g.taken.assign((size_t)numThreads, 0);
-    g.left = numThreads;
-    if (pir_engine_answer_slices(e, key, numThreads, g.parts.data()) != PIR_OK)
-      die("runOptimizedDPFTreeQueryThread");
-    st->groups.push_back(std::move(g));
-    it = st->groups.end() - 1;
+  {
+    std::lock_guard<std::mutex> lk(st->mu);
+    e = engine_for(s, st, NUM_ROUNDS);
+    if (!key || numThreads < 1 || threadNum < 0 || threadNum >= numThreads ||
+        (numThreads & (numThreads - 1)) || numThreads > NUM_ENCODED_FILES) {
+      fprintf(stderr, "pir shim: thread %d of %d (a power of two <= %d rows)\n", threadNum,
+              numThreads, NUM_ENCODED_FILES);
+      abort();
+    }
+    const size_t klen = (size_t)calcOptimizedDPFTreeKeyLength(
+        NUM_PARTIES < 2 ? 2 : NUM_PARTIES, LOG_NUM_ENCODED_FILES, NUM_ROUNDS);
+    // groups whose every slice was copied out are done
+    st->groups.erase(std::remove_if(st->groups.begin(), st->groups.end(),
+                                    [](const std::shared_ptr<SliceGroup>& x) {
+                                      return x->left.load(std::memory_order_acquire) == 0;
+                                    }),
+                     st->groups.end());
+    for (auto& x : st->groups)
+      if (x->num_threads == numThreads && !x->taken[threadNum] &&
+          memcmp(x->key.data(), key, klen) == 0) {
+        g = x;
+        break;
+      }
+    if (!g) {  // the first call of this query: it answers every slice
+      if (st->groups.size() >= kMaxSliceGroups) st->groups.erase(st->groups.begin());
+      g = std::make_shared<SliceGroup>();
+      g->key.assign(key, key + klen);
+      g->num_threads = numThreads;
+      g->parts.resize((size_t)numThreads * ans);
+      g->taken.assign((size_t)numThreads, 0);
+      g->left.store(numThreads, std::memory_order_relaxed);
+      st->groups.push_back(g);
+      pass = std::shared_lock<std::shared_mutex>(st->life);  // no exclusive holder: we hold mu
+    }
+    g->taken[threadNum] = 1;
   }
-  const uint8_t* part = it->parts.data() + (size_t)threadNum * ans;
+  if (pass.owns_lock()) {  // the one engine pass of the query, outside the server lock
+    const int rc = pir_engine_answer_slices(e, key, numThreads, g->parts.data());
+    pass.unlock();
+    {
+      std::lock_guard<std::mutex> gl(g->m);
+      g->state.store(rc == PIR_OK ? 1 : -1, std::memory_order_release);
+    }
+    g->cv.notify_all();
+  } else {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (g->state.load(std::memory_order_acquire) == 0 &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(5))
+      std::this_thread::yield();
+    if (g->state.load(std::memory_order_acquire) == 0) {
+      std::unique_lock<std::mutex> gl(g->m);
+      g->cv.wait(gl, [&] { return g->state.load(std::memory_order_acquire) != 0; });
+    }
+  }
+  if (g->state.load(std::memory_order_acquire) < 0) die("runOptimizedDPFTreeQueryThread");
+  const uint8_t* part = g->parts.data() + (size_t)threadNum * ans;
   for (int a = 0; a < NUM_ROUNDS; ++a) memcpy(result[a], part + a * efs, efs);
-  it->taken[threadNum] = 1;
-  if (--it->left == 0) st->groups.erase(it);
+  g->left.fetch_sub(1, std::memory_order_acq_rel);
 }
 
 // RunTreeQuery's fan-out (src/server_util/tree.go:60-80) for callers without Go: numThreads
