@@ -77,6 +77,12 @@ MP_CONFIGS = {
     "cm": (24, 1024, 3, 1, "multiparty sqrt(N) DPF PIR (mode 1): 2^24 x 1 KiB shard, p=3, t=1 (2 shares, 4 seeds per row of 8192 records)"),
     "cm4": (24, 1024, 4, 1, "multiparty sqrt(N) DPF PIR (mode 1): 2^24 x 1 KiB shard, p=4, t=1 (3 shares, 8 seeds per row of 8192 records)"),
 }
+# covering-design sqrt(N) DPF answers (mode 4, runCDQueryThread, server.cpp:443-492): the same
+# evaluation + scan on evalAllCDThread's layout -- (n, efs, NUM_CD_KEYS_NEEDED, NUM_CD_KEYS)
+CD_CONFIGS = {
+    "ccd": (24, 1024, 6, 3, "covering-design sqrt(N) DPF PIR (mode 4): 2^24 x 1 KiB shard, CD842 (the reference's P = 8 setup: 3 shares, 32 seeds per row of 32768 records)"),
+    "ccd7": (24, 1024, 7, 4, "covering-design sqrt(N) DPF PIR (mode 4): 2^24 x 1 KiB shard, CD732 (4 shares, 64 seeds per row of 32768 records)"),
+}
 # batched configs: a step answers `batch` keys (distinct indices) against the shard
 BATCH_CONFIGS = {
     "c3b": (24, 256, 2, 1, 128, "configs[2]: 1 MI355X, one shard 2^24 x 256 B, 128 batched queries"),
@@ -477,7 +483,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default=None,
-                    choices=sorted(CONFIGS) + sorted(BATCH_CONFIGS) + sorted(COEF_CONFIGS) + sorted(MP_CONFIGS),
+                    choices=sorted(CONFIGS) + sorted(BATCH_CONFIGS) + sorted(COEF_CONFIGS) + sorted(MP_CONFIGS) + sorted(CD_CONFIGS),
                     help="default: c24 on one GPU, c4 (split shard) on several")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=20.0,
@@ -520,7 +526,7 @@ def main():
         return run_batch(args, ctx, config)
     if config in COEF_CONFIGS:
         return run_coefs(args, ctx, config)
-    if config in MP_CONFIGS:
+    if config in MP_CONFIGS or config in CD_CONFIGS:
         return run_mp(args, ctx, config)
     n_cfg, efs, p, nq, strong, workload = CONFIGS[config]
     g = log2_exact(world)
@@ -894,41 +900,57 @@ def run_coefs(args, ctx, config):
 
 
 def run_mp(args, ctx, config):
-    """Multiparty sqrt(N) DPF answers (answer_mp_dev): each step evaluates one query's key into
-    its NUM_RSS_KEYS shares (k_mp_shares) and scans them against the shard.  Keys are random
-    bytes in the evaluation's layout (toggle bytes 0/1): the reference's own key generation
-    leaves them unset (params.cpp:613-617).  N = 1 only (replicas on more GPUs)."""
+    """Multiparty (MP_CONFIGS) or covering-design (CD_CONFIGS) sqrt(N) DPF answers
+    (answer_mp_dev / answer_cd_dev): each step evaluates one query's key into its shares
+    (k_mp_shares) and scans them against the shard.  Keys are random bytes in the evaluation's
+    layout (toggle bytes 0/1): the reference's multiparty key generation leaves them unset
+    (params.cpp:613-617); its CD key generation is client code outside the server path
+    (tests/test_cd.py pins the engine on genCDDPF's own keys).  N = 1 only (replicas on more
+    GPUs)."""
     import erasurecodedpir_amd as pir
-    n, efs, p, t, workload = MP_CONFIGS[config]
+    cd = config in CD_CONFIGS
+    if cd:
+        n, efs, qn, nrk, workload = CD_CONFIGS[config]
+        eb = pir.cd_key_len(0, n, 0, qn, nrk)
+        mu, p2 = 1 << (n // 2 + 3), 1 << (qn - 1)
+    else:
+        n, efs, p, t, workload = MP_CONFIGS[config]
+        nrk = pir.mp_num_keys(p, t)
+        eb = pir.mp_eval_bytes(p, n, t)
+        mu = 1 << int(np.ceil(np.log2(np.ceil(2 ** (n / 2) * 2 ** ((p - 1) / 2)))))
+        p2 = 1 << (math.comb(p, t) - 1)
     N = 1 << n
-    nrk = pir.mp_num_keys(p, t)
-    eb = pir.mp_eval_bytes(p, n, t)
     rng = np.random.default_rng(11)
     K, W = args.steps, args.warmup
     nkeys = max(2, min(K, 4))
-    mu = 1 << int(np.ceil(np.log2(np.ceil(2 ** (n / 2) * 2 ** ((p - 1) / 2)))))
-    nu, p2 = N // mu, 1 << (math.comb(p, t) - 1)
+    nu = N // mu
     tog = nu * 16 * p2
     keys = rng.integers(0, 256, (nkeys, eb), dtype=np.uint8)
     keys[:, tog:tog + nrk * nu * p2] = rng.integers(0, 2, (nkeys, nrk * nu * p2), dtype=np.uint8)
+    if cd:
+        ans_dev = lambda dk, dr: eng.answer_cd_dev(dk, qn, nrk, dr)  # noqa: E731
+        ans = lambda k: eng.answer_cd(k, qn, nrk)  # noqa: E731
+    else:
+        ans_dev = lambda dk, dr: eng.answer_mp_dev(dk, p, t, dr)  # noqa: E731
+        ans = lambda k: eng.answer_mp(k, p, t)  # noqa: E731
     eng = pir.Engine(2, 1, n, efs, nrk, device=ctx.local)
     eng.fill_shard_random(SHARD_SEED)
     d_k = eng.alloc_dev(nkeys * eb)
     d_r = eng.alloc_dev(K * nrk * efs)
     eng.h2d(d_k, keys.reshape(-1))
     for i in range(W):
-        eng.answer_mp_dev(d_k + (i % nkeys) * eb, p, t, d_r)
-    dt = ctx.timed(eng, lambda: [eng.answer_mp_dev(d_k + (i % nkeys) * eb, p, t,
-                                                   d_r + i * nrk * efs) for i in range(K)])
+        ans_dev(d_k + (i % nkeys) * eb, d_r)
+    dt = ctx.timed(eng, lambda: [ans_dev(d_k + (i % nkeys) * eb, d_r + i * nrk * efs)
+                                 for i in range(K)])
     ms = dt / K * 1e3
     # correctness at full size: flipping cw[j][x] by d moves share a's answer by
     # d * XOR of the records i*mu + x of the rows whose toggle (a, i, j) is set
     j, x, d = 1, 777, 0x5A
     cwo = tog + nrk * nu * p2
     k0 = keys[0].copy()
-    base = eng.answer_mp(k0, p, t)
+    base = ans(k0)
     k0[cwo + j * mu + x] ^= d
-    moved = eng.answer_mp(k0, p, t)
+    moved = ans(k0)
     tab = _gf_table(d)
     ok = True
     for a in range(nrk):
@@ -938,15 +960,16 @@ def run_mp(args, ctx, config):
                 acc ^= eng.shard_row(i * mu + x)
         ok &= bool(np.array_equal((base ^ moved)[a], tab[acc]))
     dev0 = eng.d2h(d_r, nrk * efs).reshape(nrk, efs)
-    ok_dev = bool(np.array_equal(dev0, eng.answer_mp(keys[0], p, t)))
+    ok_dev = bool(np.array_equal(dev0, ans(keys[0])))
     eng.close()
     gib = float(N) * efs / GIB
     algo = float(N) * efs + eb  # shard + the key
     out = {"metric": METRIC, "value": round(gib / (ms / 1e3), 3), "unit": "GiB/s", "n_gpus": 1,
            "steps": K, "warmup": W, "ms_per_step": r5(ms), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-           "config": {"workload": workload, "records": N, "record_bytes": efs, "parties": p,
-                      "threshold": t, "shares": nrk, "seeds_per_row": p2, "row_records": mu,
+           "config": {"workload": workload, "records": N, "record_bytes": efs,
+                      **({"num_cd_keys_needed": qn} if cd else {"parties": p, "threshold": t}),
+                      "shares": nrk, "seeds_per_row": p2, "row_records": mu,
                       "rows": nu, "key_bytes_read": eb,
                       "step": "one query: k_mp_shares (AES-CTR per seed, toggled into the shares) "
                               "+ k_scan + k_reduce"},

@@ -7,7 +7,7 @@ reference's server.h entry points (include/pir_server.h).
 """
 from ._lib import LIB_PATH, PirError, load  # noqa: F401
 from .client import final_cw, gen_keys  # noqa: F401
-from .engine import Engine, comm_unique_id, key_len, mp_eval_bytes, mp_key_len, mp_num_keys  # noqa: F401
+from .engine import Engine, cd_key_len, comm_unique_id, key_len, mp_eval_bytes, mp_key_len, mp_num_keys  # noqa: F401
 
-__all__ = ["Engine", "gen_keys", "final_cw", "key_len", "mp_num_keys", "mp_key_len", "mp_eval_bytes", "comm_unique_id", "load", "LIB_PATH",
+__all__ = ["Engine", "gen_keys", "final_cw", "key_len", "mp_num_keys", "mp_key_len", "mp_eval_bytes", "cd_key_len", "comm_unique_id", "load", "LIB_PATH",
            "PirError"]

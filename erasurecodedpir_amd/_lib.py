@@ -89,6 +89,9 @@ PROTOTYPES = {
     "pir_engine_answer_mp_dev": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     "pir_engine_mp_num_keys": (_I, [_I, _I]),
     "pir_engine_mp_key_len": (_I, [_I, _I, _I]),
+    "pir_engine_answer_cd": (_I, [_P, _P, _U64, _I, _I, _I, _I, _P]),
+    "pir_engine_answer_cd_dev": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
+    "pir_engine_cd_key_len": (_I, [_I, _I, _I, _I, _I]),
     "pir_engine_mp_eval_bytes": (ctypes.c_longlong, [_I, _I, _I]),
     "pir_engine_answer_dev": (_I, [_P, _P, _P, _P]),
     "pir_engine_answer_batch_dev": (_I, [_P, _P, _I, _P, _P]),

@@ -784,16 +784,68 @@ int answer_mp_locked(pir_engine* e, const pir::MpLayout& L, const uint8_t* d_key
   return PIR_OK;
 }
 
+// the layout's share count against the engine's rounds, the thread slot
+int check_layout(const pir_engine* e, const pir::MpLayout& L, int thread_num, int num_threads,
+                 const char* what) {
+  if (L.nrk != e->cfg.num_rounds)
+    return fail(PIR_EINVAL, "the %s layout gives %d shares but the engine has %d rounds", what,
+                L.nrk, e->cfg.num_rounds);
+  if (num_threads < 1 || thread_num < 0 || thread_num >= num_threads)
+    return fail(PIR_EINVAL, "thread_num %d of %d", thread_num, num_threads);
+  return PIR_OK;
+}
+
 int check_mp(const pir_engine* e, int p, int t, int thread_num, int num_threads,
              pir::MpLayout* L) {
   if (!pir::mp_layout(p, e->cfg.log_num_records, t, L))
     return fail(PIR_EINVAL, "no multiparty DPF layout for p=%d t=%d n=%d", p, t,
                 e->cfg.log_num_records);
-  if (L->nrk != e->cfg.num_rounds)
-    return fail(PIR_EINVAL, "p=%d t=%d gives %d shares (NUM_RSS_KEYS) but the engine has %d rounds",
-                p, t, L->nrk, e->cfg.num_rounds);
-  if (num_threads < 1 || thread_num < 0 || thread_num >= num_threads)
-    return fail(PIR_EINVAL, "thread_num %d of %d", thread_num, num_threads);
+  return check_layout(e, *L, thread_num, num_threads, "multiparty (NUM_RSS_KEYS)");
+}
+
+int check_cd(const pir_engine* e, int q_needed, int num_cd_keys, int thread_num,
+             int num_threads, pir::MpLayout* L) {
+  if (!pir::cd_layout(e->cfg.log_num_records, q_needed, num_cd_keys, L))
+    return fail(PIR_EINVAL, "no covering-design DPF layout for NUM_CD_KEYS_NEEDED=%d "
+                "NUM_CD_KEYS=%d n=%d", q_needed, num_cd_keys, e->cfg.log_num_records);
+  return check_layout(e, *L, thread_num, num_threads, "covering-design (NUM_CD_KEYS)");
+}
+
+// a validated sqrt(N) layout's answer from a device key (any alignment)
+int answer_layout_dev(pir_engine* e, const pir::MpLayout& L, const uint8_t* d_key, int thread_num,
+                      int num_threads, uint8_t* d_result, void* stream) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  if (int rc = ws_acquire(e, s)) return rc;
+  if (((uintptr_t)d_key & 15) && L.eval_bytes) {  // the seeds are read as 16-byte words
+    if (int rc = ensure_buf(&e->d_mpkey, &e->mpkey_cap, L.eval_bytes)) return rc;
+    HIP_TRY(hipMemcpyAsync(e->d_mpkey, d_key, L.eval_bytes, hipMemcpyDeviceToDevice, s));
+    d_key = e->d_mpkey;
+  }
+  return ws_release(e, s, answer_mp_locked(e, L, d_key, thread_num, num_threads, d_result, s));
+}
+
+// ... and from a host key of key_bytes bytes, answer copied back to host memory
+int answer_layout_host(pir_engine* e, const pir::MpLayout& L, const uint8_t* key,
+                       uint64_t key_bytes, int thread_num, int num_threads, uint8_t* result,
+                       const char* what) {
+  if (key_bytes < L.eval_bytes)
+    return fail(PIR_EINVAL, "%s key of %llu bytes; the evaluation reads %llu", what,
+                (unsigned long long)key_bytes, (unsigned long long)L.eval_bytes);
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const size_t out_bytes = (size_t)e->cfg.num_rounds * e->cfg.record_bytes;
+  if (int rc = ws_acquire(e, e->stream)) return rc;
+  if (int rc = ensure_buf(&e->d_mpkey, &e->mpkey_cap, std::max<uint64_t>(16, L.eval_bytes))) return rc;
+  if (L.eval_bytes)
+    HIP_TRY(hipMemcpyAsync(e->d_mpkey, key, L.eval_bytes, hipMemcpyHostToDevice, e->stream));
+  int rc = ws_release(e, e->stream, answer_mp_locked(e, L, e->d_mpkey, thread_num, num_threads,
+                                                     e->d_result, e->stream));
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(e->h_res, e->d_result, out_bytes, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memcpy(result, e->h_res, out_bytes);
   return PIR_OK;
 }
 
@@ -1210,16 +1262,7 @@ int pir_engine_answer_mp_dev(pir_engine_t* e, const uint8_t* d_key, int p, int t
   if (int rc = check_key_ptr(d_key)) return rc;
   pir::MpLayout L;
   if (int rc = check_mp(e, p, t, thread_num, num_threads, &L)) return rc;
-  std::lock_guard<std::mutex> lk(e->mu);
-  HIP_TRY(hipSetDevice(e->cfg.device));
-  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  if (int rc = ws_acquire(e, s)) return rc;
-  if (((uintptr_t)d_key & 15) && L.eval_bytes) {  // the seeds are read as 16-byte words
-    if (int rc = ensure_buf(&e->d_mpkey, &e->mpkey_cap, L.eval_bytes)) return rc;
-    HIP_TRY(hipMemcpyAsync(e->d_mpkey, d_key, L.eval_bytes, hipMemcpyDeviceToDevice, s));
-    d_key = e->d_mpkey;
-  }
-  return ws_release(e, s, answer_mp_locked(e, L, d_key, thread_num, num_threads, d_result, s));
+  return answer_layout_dev(e, L, d_key, thread_num, num_threads, d_result, stream);
 }
 
 int pir_engine_answer_mp(pir_engine_t* e, const uint8_t* key, uint64_t key_bytes, int p, int t,
@@ -1228,23 +1271,34 @@ int pir_engine_answer_mp(pir_engine_t* e, const uint8_t* key, uint64_t key_bytes
   if (int rc = check_key_ptr(key)) return rc;
   pir::MpLayout L;
   if (int rc = check_mp(e, p, t, thread_num, num_threads, &L)) return rc;
-  if (key_bytes < L.eval_bytes)
-    return fail(PIR_EINVAL, "multiparty key of %llu bytes; the evaluation reads %llu",
-                (unsigned long long)key_bytes, (unsigned long long)L.eval_bytes);
-  std::lock_guard<std::mutex> lk(e->mu);
-  HIP_TRY(hipSetDevice(e->cfg.device));
-  const size_t out_bytes = (size_t)e->cfg.num_rounds * e->cfg.record_bytes;
-  if (int rc = ws_acquire(e, e->stream)) return rc;
-  if (int rc = ensure_buf(&e->d_mpkey, &e->mpkey_cap, std::max<uint64_t>(16, L.eval_bytes))) return rc;
-  if (L.eval_bytes)
-    HIP_TRY(hipMemcpyAsync(e->d_mpkey, key, L.eval_bytes, hipMemcpyHostToDevice, e->stream));
-  int rc = ws_release(e, e->stream, answer_mp_locked(e, L, e->d_mpkey, thread_num, num_threads,
-                                                     e->d_result, e->stream));
-  if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(e->h_res, e->d_result, out_bytes, hipMemcpyDeviceToHost, e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  memcpy(result, e->h_res, out_bytes);
-  return PIR_OK;
+  return answer_layout_host(e, L, key, key_bytes, thread_num, num_threads, result, "multiparty");
+}
+
+int pir_engine_cd_key_len(int p, int n, int t, int num_cd_keys_needed, int num_cd_keys) {
+  (void)p; (void)t;  // utils.cpp:118-129 takes them and does not use them
+  pir::MpLayout L;
+  return pir::cd_layout(n, num_cd_keys_needed, num_cd_keys, &L) ? (int)L.eval_bytes : 0;
+}
+
+int pir_engine_answer_cd_dev(pir_engine_t* e, const uint8_t* d_key, int num_cd_keys_needed,
+                             int num_cd_keys, int thread_num, int num_threads, uint8_t* d_result,
+                             void* stream) {
+  if (!e || !d_result) return fail(PIR_EINVAL, "null argument");
+  if (int rc = check_key_ptr(d_key)) return rc;
+  pir::MpLayout L;
+  if (int rc = check_cd(e, num_cd_keys_needed, num_cd_keys, thread_num, num_threads, &L)) return rc;
+  return answer_layout_dev(e, L, d_key, thread_num, num_threads, d_result, stream);
+}
+
+int pir_engine_answer_cd(pir_engine_t* e, const uint8_t* key, uint64_t key_bytes,
+                         int num_cd_keys_needed, int num_cd_keys, int thread_num, int num_threads,
+                         uint8_t* result) {
+  if (!e || !result) return fail(PIR_EINVAL, "null argument");
+  if (int rc = check_key_ptr(key)) return rc;
+  pir::MpLayout L;
+  if (int rc = check_cd(e, num_cd_keys_needed, num_cd_keys, thread_num, num_threads, &L)) return rc;
+  return answer_layout_host(e, L, key, key_bytes, thread_num, num_threads, result,
+                            "covering-design");
 }
 
 int pir_engine_answer_slice(pir_engine_t* e, const uint8_t* key, int thread_num, int num_threads,

@@ -30,6 +30,10 @@ struct MpLayout {
 int mp_choose(int n, int k);
 // false when the parameters give no usable layout (t < 1, t >= p, too many seeds/shares)
 bool mp_layout(int p, int n, int t, MpLayout* out);
+// the covering-design layout of evalAllCDThread (multiparty_dpf.cpp:617-690): nrk = NUM_CD_KEYS
+// shares, p2 = 2^(NUM_CD_KEYS_NEEDED - 1) seeds per row, mu = 2^(n/2 + 3) (integer n / 2), the
+// same key sections (p, t unused: 0)
+bool cd_layout(int n, int q_needed, int num_cd_keys, MpLayout* out);
 
 // d_c[(r - rec_lo) * nrp + a] = share[a][r] (0 for a >= nrk) for records r in [rec_lo, rec_hi)
 // (row-aligned or 16-aligned bounds not required); d_key: the raw key, eval_bytes long

@@ -39,6 +39,22 @@ bool mp_layout(int p, int n, int t, MpLayout* L) {
   return L->nrk >= 1;
 }
 
+bool cd_layout(int n, int q_needed, int num_cd_keys, MpLayout* L) {
+  *L = MpLayout{};
+  if (n < 0 || n > 40 || q_needed < 1 || q_needed > 31 || num_cd_keys < 1 || num_cd_keys > 16)
+    return false;
+  L->n = n;
+  L->nrk = num_cd_keys;
+  L->p2 = 1u << (q_needed - 1);
+  L->mu_pow = n / 2 + 3;  // ceil((double)(n/2)) + 3: integer n / 2
+  L->mu = 1ull << L->mu_pow;
+  L->nu = L->mu_pow > n ? 0 : 1ull << (n - L->mu_pow);
+  L->tog_off = L->nu * 16ull * L->p2;
+  L->cw_off = L->tog_off + (uint64_t)L->nrk * L->nu * L->p2;
+  L->eval_bytes = L->cw_off + (uint64_t)L->p2 * L->mu;
+  return true;
+}
+
 namespace {
 
 __device__ __forceinline__ uint32_t byte_of(uint4 v, int k) {

@@ -14,6 +14,11 @@
 //                            Results, ServerLatency, ReceiveTime, SendTime}  (hollanti.go:16-112,
 //                            Mode 3: explicit coefficient vectors scanned on the GPU; the shard
 //                            encoded within files, client.cpp:99-103, on the host)
+//   CD732_SEARCH_REQUEST (5)  CD732SearchRequest{Key} -> CD732SearchResponse{Results,
+//                            ServerLatency, ReceiveTime, SendTime}  (cd732.go:16-100, Mode 4: the
+//                            covering-design key's NUM_CD_KEYS shares scanned on the GPU; the
+//                            reference's handler also frees the server after every query,
+//                            cd732.go:96 -- not inherited)
 //   TEST_REQUEST (7)         TestRequest{Msg} -> TestResponse{Msg}
 // Structs travel as msgpack maps keyed by the Go field names (the go-msgpack MsgpackHandle
 // default).  Durations are int64 nanoseconds; times are msgpack timestamp extensions (-1).
@@ -53,7 +58,7 @@ namespace {
 
 enum : uint8_t {  // common.go:147-154
   SETUP_REQUEST = 0, TREE_SEARCH_REQUEST = 1, MULTIPARTY_SEARCH_REQUEST = 3,
-  HOLLANTI_SEARCH_REQUEST = 4, TEST_REQUEST = 7
+  HOLLANTI_SEARCH_REQUEST = 4, CD732_SEARCH_REQUEST = 5, TEST_REQUEST = 7
 };
 
 // ---- msgpack (the subset the protocol uses) ----------------------------------------------
@@ -247,8 +252,8 @@ struct Server {
   std::mutex mu;
   pir_engine_t* eng = nullptr;
   // of the current engine (the params globals may move on): mode, answer rows, record bytes,
-  // tree key length, multiparty (p, t), Hollanti coefficient-vector length
-  int mode = -1, nq = 0, efs = 0, key_len = 0, p = 0, t = 0;
+  // tree key length, multiparty (p, t), NUM_CD_KEYS_NEEDED, Hollanti coefficient-vector length
+  int mode = -1, nq = 0, efs = 0, key_len = 0, p = 0, t = 0, cd_needed = 0;
   uint64_t num_files = 0;
 };
 Server g;
@@ -258,8 +263,9 @@ std::string setup(const MVal& req) {  // server.go:295-331
   const int t = (int)req.get_int("T", 1), k = (int)req.get_int("K", 1), r = (int)req.get_int("R");
   const int b = (int)req.get_int("B"), rho = (int)req.get_int("Rho", 1);
   const int mode = (int)req.get_int("Mode"), mac = (int)req.get_int("CheckMAC");
-  if (mode != 0 && mode != 1 && mode != 3)
-    return "only the tree (0), multiparty (1) and Hollanti (3) modes are served by this engine";
+  if (mode != 0 && mode != 1 && mode != 3 && mode != 4)
+    return "only the tree (0), multiparty (1), Hollanti (3) and covering-design (4) modes are "
+           "served by this engine";
   if (mac != 0) return "CheckMAC setups are outside this engine's scope";
   if (mode == 0 && (t != 1 || b != 0)) return "tree mode needs T = 1 and B = 0";
   if (mode == 1 && t < 1) return "multiparty mode needs T >= 1";
@@ -274,11 +280,12 @@ std::string setup(const MVal& req) {  // server.go:295-331
   g.mode = -1;
   setSystemParams(log_files, fsz, t, k, r, b, rho, mac, mode);
   if (g.party > NUM_PARTIES) return "this server's party index exceeds NUM_PARTIES";
-  const int rounds = mode == 1 ? NUM_RSS_KEYS : NUM_ROUNDS;
-  if (rounds < 1 || rounds > PIR_MAX_ROUNDS) return "answer rows outside [1,16] (NUM_ROUNDS / NUM_RSS_KEYS)";
+  const int rounds = mode == 1 ? NUM_RSS_KEYS : (mode == 4 ? NUM_CD_KEYS : NUM_ROUNDS);
+  if (rounds < 1 || rounds > PIR_MAX_ROUNDS)
+    return "answer rows outside [1,16] (NUM_ROUNDS / NUM_RSS_KEYS / NUM_CD_KEYS)";
   pir_engine_config c{};
   c.device = g.device;
-  // the party count only sizes tree-DPF keys (modes 1 and 3 answer other key forms)
+  // the party count only sizes tree-DPF keys (modes 1, 3 and 4 answer other key forms)
   c.num_parties = mode == 0 ? NUM_PARTIES : 2;
   c.party_index = mode == 0 ? g.party : 1;
   c.log_num_records = LOG_NUM_ENCODED_FILES;
@@ -302,6 +309,7 @@ std::string setup(const MVal& req) {  // server.go:295-331
   g.efs = ENCODED_FILE_SIZE_BYTES;
   g.p = NUM_PARTIES;
   g.t = T;
+  g.cd_needed = NUM_CD_KEYS_NEEDED;
   g.num_files = (uint64_t)NUM_FILES;
   g.key_len = pir_engine_key_len(c.num_parties, c.log_num_records, c.num_rounds);
   return "";
@@ -353,7 +361,8 @@ void handle(SSL* ssl) {
       w.integer(std::chrono::duration_cast<std::chrono::nanoseconds>(
                     std::chrono::steady_clock::now() - t0).count());
     } else if (type == TREE_SEARCH_REQUEST || type == MULTIPARTY_SEARCH_REQUEST ||
-               type == HOLLANTI_SEARCH_REQUEST) {  // tree.go:17-101, multiparty.go, hollanti.go
+               type == HOLLANTI_SEARCH_REQUEST || type == CD732_SEARCH_REQUEST) {
+      // tree.go:17-101, multiparty.go, hollanti.go, cd732.go
       const MVal* key = req.get("Key");
       std::vector<uint8_t> out;
       int nq = 0, efs = 0;  // this answer's shape, read under the lock with the engine
@@ -362,7 +371,9 @@ void handle(SSL* ssl) {
         nq = g.nq;
         efs = g.efs;
         out.resize((size_t)nq * efs);
-        const int want = type == TREE_SEARCH_REQUEST ? 0 : (type == MULTIPARTY_SEARCH_REQUEST ? 1 : 3);
+        const int want = type == TREE_SEARCH_REQUEST ? 0
+                         : type == MULTIPARTY_SEARCH_REQUEST ? 1
+                         : type == CD732_SEARCH_REQUEST ? 4 : 3;
         int rc = PIR_OK;
         if (!g.eng) {
           err = "query before setup";
@@ -379,6 +390,12 @@ void handle(SSL* ssl) {
           else
             rc = pir_engine_answer_mp(g.eng, (const uint8_t*)key->s.data(), key->s.size(), g.p,
                                       g.t, 0, 1, out.data());
+        } else if (type == CD732_SEARCH_REQUEST) {  // the Thread slices of cd732.go:61-76, XORed
+          if (!is_bytes(key))
+            err = "bad key";
+          else
+            rc = pir_engine_answer_cd(g.eng, (const uint8_t*)key->s.data(), key->s.size(),
+                                      g.cd_needed, nq, 0, 1, out.data());
         } else {  // Key [][]byte: NUM_ROUNDS coefficient vectors of NUM_FILES bytes
           std::vector<const uint8_t*> ptrs;
           if (key && key->kind == MVal::ARR && (int)key->a.size() == nq)

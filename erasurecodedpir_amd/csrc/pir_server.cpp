@@ -49,9 +49,9 @@ int IS_HERMITE = 0;
 int D = 0;
 int MAC_SIZE_BYTES = 32;
 int CHECK_MAC = 0;
-int NUM_RSS_KEYS = 0;  // params.cpp:39-46 defaults (CD / Woodruff modes are not served)
-int NUM_CD_KEYS = 0;
-int NUM_CD_KEYS_NEEDED = 0;
+int NUM_RSS_KEYS = 0;  // params.cpp:39-46 defaults (Woodruff mode is not served)
+int NUM_CD_KEYS = 2;   // params.cpp:368-369: the CD532 counts until a covering design is chosen
+int NUM_CD_KEYS_NEEDED = 4;
 int WOODRUFF_M = 0;
 int WOODRUFF_D = 0;
 int WOODRUFF_DERIVATIVE = 0;
@@ -554,18 +554,39 @@ int calcOptimizedDPFTreeKeyLength(int p, int log_domainSize, int numQueries) {
   return pir_engine_key_len(p, log_domainSize, numQueries);
 }
 
-// params.cpp:372 isRss: cleared for good by the covering-design setups of params.cpp:520-599
-// (with the default M = 4 only the T = 2, p = 12 / 14 / 16 ones apply)
-static bool g_is_rss = true;
+// params.cpp:12 `int M = 4` (the covering designs' extra-party count) and params.cpp:372 isRss:
+// setModeParams(CD) sets M to 2 for K = 2, B = 1 (params.cpp:439-441) and a covering-design
+// selection clears isRss (:520-599); the reference never resets either, so a later setup's party
+// count and NUM_RSS_KEYS depend on the process's call history.  This shim starts every
+// setSystemParams from M = 4, isRss = 1, as a fresh process would (the Go servers set their
+// parameters once).
+static int g_cd_m = 4;
+
+// The covering designs of params.cpp:519-599: (T, NUM_PARTIES, M) -> NUM_CD_KEYS,
+// NUM_CD_KEYS_NEEDED (the counts of params.cpp:64-362); every mode runs this selection.
+static bool select_covering(int t, int p, int m) {
+  static const int tab[][5] = {  // p, M, NUM_CD_KEYS, NUM_CD_KEYS_NEEDED  (all with T == 2)
+      {5, 1, 2, 4}, {7, 1, 4, 7}, {6, 1, 3, 6}, {8, 1, 7, 11}, {9, 1, 8, 12}, {8, 2, 3, 6},
+      {9, 2, 5, 8}, {10, 2, 6, 9}, {12, 4, 3, 6}, {16, 4, 3, 6}, {14, 4, 3, 6}};
+  if (t != 2) return false;
+  for (const auto& c : tab)
+    if (c[0] == p && c[1] == m) {
+      NUM_CD_KEYS = c[2];
+      NUM_CD_KEYS_NEEDED = c[3];
+      return true;
+    }
+  return false;
+}
 
 // params.cpp:467-512 with setModeParams(Tree) (params.cpp:414-418), setModeParams(Multiparty)
-// (:419-422) or setModeParams(Hollanti) (:430-433), and the RSS share count of :603-619; the
-// other modes (Shamir, CD, Woodruff, Goldberg) abort
+// (:419-422), setModeParams(Hollanti) (:430-433) or setModeParams(CD) (:434-447), the covering
+// design of :519-599 and the RSS share count of :603-619; the other modes (Shamir, Woodruff,
+// Goldberg) abort
 void setSystemParams(int logNumFiles, int fileSizeBytes, int t, int k, int r, int b, int rho,
                      int checkMac, int mode) {
-  if (mode != 0 && mode != 1 && mode != 3) {
+  if (mode != 0 && mode != 1 && mode != 3 && mode != 4) {
     fprintf(stderr, "pir shim: mode %d is outside the engine's scope (tree = 0, multiparty = 1, "
-            "Hollanti = 3)\n", mode);
+            "Hollanti = 3, covering design = 4)\n", mode);
     abort();
   }
   if (mode == 0 && t != 1) {  // params.cpp:415 assert(T == 1)
@@ -583,7 +604,21 @@ void setSystemParams(int logNumFiles, int fileSizeBytes, int t, int k, int r, in
   FILE_SIZE_BYTES = (uint32_t)fileSizeBytes;
   CHECK_MAC = checkMac;
   MODE = mode;
-  NUM_PARTIES = K + R + T + 2 * B + (mode == 1 ? 0 : RHO - 1);
+  g_cd_m = 4;
+  if (mode == 4) {
+    if (K == 4 && B == 2) {
+      NUM_PARTIES = 16;
+    } else if (K == 3 && B == 2) {
+      NUM_PARTIES = 14;
+    } else if (K == 2 && B == 1) {
+      g_cd_m = 2;
+      NUM_PARTIES = 8;
+    } else {
+      NUM_PARTIES = T + K + R + 2 * B + g_cd_m;
+    }
+  } else {
+    NUM_PARTIES = K + R + T + 2 * B + (mode == 1 ? 0 : RHO - 1);
+  }
   ENCODE_ACROSS = mode == 3 ? 0 : 1;
   NUM_RESPONSES = NUM_PARTIES - R;
   if (ENCODE_ACROSS) {
@@ -602,8 +637,8 @@ void setSystemParams(int logNumFiles, int fileSizeBytes, int t, int k, int r, in
     ENCODED_FILE_SIZE_BYTES = (int)((FILE_SIZE_BYTES + k - 1) / k);
   }
   NUM_ROUNDS = (K == 1) ? 1 : K / RHO;
-  if (T == 2 && (NUM_PARTIES == 12 || NUM_PARTIES == 14 || NUM_PARTIES == 16)) g_is_rss = false;
-  if (t >= 1 && g_is_rss) NUM_RSS_KEYS = pir_engine_mp_num_keys(NUM_PARTIES, T);
+  const bool is_rss = !select_covering(T, NUM_PARTIES, g_cd_m);
+  if (t >= 1 && is_rss) NUM_RSS_KEYS = pir_engine_mp_num_keys(NUM_PARTIES, T);
 }
 
 // utils.cpp:105-116
@@ -884,8 +919,20 @@ void assembleWoodruffQueryThreadResults(server* s, uint8_t*** in, int numThreads
 void runOptShamirDPFQueryThread(server*, uint8_t**, int, int, int, uint8_t**) {
   out_of_scope("runOptShamirDPFQueryThread", "Shamir");
 }
-void runCDQueryThread(server*, uint8_t*, int, int, uint8_t**) {
-  out_of_scope("runCDQueryThread", "covering-design");
+// server.cpp:443-492 (both branches compute the honest answer): NUM_CD_KEYS shares of the
+// covering-design key evaluated on the thread's rows and scanned on the engine
+void runCDQueryThread(server* s, uint8_t* key, int threadNum, int numThreads, uint8_t** result) {
+  ShimState* st = state_of(s);
+  std::lock_guard<std::mutex> lk(st->mu);
+  pir_engine_t* e = engine_for(s, st, NUM_CD_KEYS);
+  const size_t efs = (size_t)ENCODED_FILE_SIZE_BYTES;
+  std::vector<uint8_t> out((size_t)NUM_CD_KEYS * efs);
+  const int kl = calcCDDPFKeyLength(NUM_PARTIES, LOG_NUM_ENCODED_FILES, T, NUM_CD_KEYS_NEEDED,
+                                    NUM_CD_KEYS);
+  if (pir_engine_answer_cd(e, key, (uint64_t)(kl > 0 ? kl : 0), NUM_CD_KEYS_NEEDED, NUM_CD_KEYS,
+                           threadNum, numThreads, out.data()) != PIR_OK)
+    die("runCDQueryThread");
+  for (int a = 0; a < NUM_CD_KEYS; ++a) memcpy(result[a], out.data() + a * efs, efs);
 }
 void runWoodruffQueryThread(server*, uint8_t*, int, int, int, uint8_t**) {
   out_of_scope("runWoodruffQueryThread", "Woodruff");

@@ -234,6 +234,26 @@ class Engine:
         check(self._lib.pir_engine_answer_mp_dev(self._h, d_key, p, t, thread_num, num_threads,
                                                  d_result, stream), "answer_mp_dev")
 
+    def answer_cd(self, key, num_cd_keys_needed, num_cd_keys, thread_num=0, num_threads=1):
+        """Covering-design sqrt(N) DPF answer (runCDQueryThread, src/c/server.cpp:443-492): the
+        key's NUM_CD_KEYS shares (evalAllCDThread's layout, multiparty_dpf.cpp:617-690) scanned
+        against the shard.  The engine's num_rounds must be num_cd_keys.
+        -> (num_rounds, record_bytes)."""
+        k = np.frombuffer(bytes(key), np.uint8) if not isinstance(key, np.ndarray) else \
+            np.ascontiguousarray(key, np.uint8)
+        out = np.empty((self.num_rounds, self.record_bytes), np.uint8)
+        check(self._lib.pir_engine_answer_cd(self._h, k.ctypes.data_as(ctypes.c_void_p), k.size,
+                                             num_cd_keys_needed, num_cd_keys, thread_num,
+                                             num_threads, out.ctypes.data_as(ctypes.c_void_p)),
+              "pir_engine_answer_cd")
+        return out
+
+    def answer_cd_dev(self, d_key, num_cd_keys_needed, num_cd_keys, d_result, thread_num=0,
+                      num_threads=1, stream=None):
+        check(self._lib.pir_engine_answer_cd_dev(self._h, d_key, num_cd_keys_needed, num_cd_keys,
+                                                 thread_num, num_threads, d_result, stream),
+              "answer_cd_dev")
+
     def eval_all(self, key):
         """(num_rounds, rows) DPF shares dataShare[a][i]."""
         k, kp = self._check_key(key)
@@ -359,6 +379,11 @@ def mp_num_keys(p, t):
 def mp_key_len(p, n, t):
     """calcMultiPartyOptDPFKeyLength (utils.cpp:105-116)."""
     return _lib.load().pir_engine_mp_key_len(p, n, t)
+
+
+def cd_key_len(p, n, t, num_cd_keys_needed, num_cd_keys):
+    """calcCDDPFKeyLength (utils.cpp:118-129) = the bytes evalAllCDThread reads; 0: no layout."""
+    return _lib.load().pir_engine_cd_key_len(p, n, t, num_cd_keys_needed, num_cd_keys)
 
 
 def mp_eval_bytes(p, n, t):

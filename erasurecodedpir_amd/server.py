@@ -136,6 +136,22 @@ class Server:
                                                            _row_ptrs(out))
         return out
 
+    def runCDQueryThread(self, key, threadNum, numThreads):
+        """Covering-design answer over thread threadNum's rows (server.cpp:443-492):
+        (NUM_CD_KEYS, EFS)."""
+        efs = _lib.global_int("ENCODED_FILE_SIZE_BYTES")
+        out = np.zeros((_lib.global_int("NUM_CD_KEYS"), efs), np.uint8)
+        k = np.frombuffer(bytes(key), np.uint8).copy()
+        need = calcCDDPFKeyLength(_lib.global_int("NUM_PARTIES"),
+                                  _lib.global_int("LOG_NUM_ENCODED_FILES"), _lib.global_int("T"),
+                                  _lib.global_int("NUM_CD_KEYS_NEEDED"),
+                                  _lib.global_int("NUM_CD_KEYS"))
+        if k.size < need:  # the shim reads calcCDDPFKeyLength bytes
+            raise ValueError(f"covering-design key of {k.size} bytes, expected {need}")
+        self._lib.runCDQueryThread(ctypes.byref(self.s), k.ctypes.data_as(ctypes.c_void_p),
+                                   threadNum, numThreads, _row_ptrs(out))
+        return out
+
     def freeServer(self):
         if self.s.ctx:
             self._lib.freeServer(ctypes.byref(self.s))
@@ -170,6 +186,16 @@ def assembleHollantiQueryThreadResults(server, parts):
 def assembleMultipartyDPFQueryThreadResults(server, parts):
     """parts: (numThreads, NUM_RSS_KEYS, EFS) -> (NUM_RSS_KEYS, EFS) (server.cpp:432-441)."""
     return _assemble("assembleMultipartyDPFQueryThreadResults", server, parts)
+
+
+def assembleCDQueryThreadResults(server, parts):
+    """parts: (numThreads, NUM_CD_KEYS, EFS) -> (NUM_CD_KEYS, EFS) (server.cpp:494-503)."""
+    return _assemble("assembleCDQueryThreadResults", server, parts)
+
+
+def calcCDDPFKeyLength(p, log_domain_size, t, num_cd_keys_needed, num_cd_keys):
+    """utils.cpp:118-129."""
+    return _lib.load().calcCDDPFKeyLength(p, log_domain_size, t, num_cd_keys_needed, num_cd_keys)
 
 
 def calcMultiPartyOptDPFKeyLength(p, log_domain_size, t):

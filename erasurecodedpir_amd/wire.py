@@ -15,8 +15,8 @@ import msgpack
 import numpy as np
 
 # common.go:147-154
-SETUP_REQUEST, TREE_SEARCH_REQUEST, MULTIPARTY_SEARCH_REQUEST, HOLLANTI_SEARCH_REQUEST, TEST_REQUEST = \
-    0, 1, 3, 4, 7
+SETUP_REQUEST, TREE_SEARCH_REQUEST, MULTIPARTY_SEARCH_REQUEST, HOLLANTI_SEARCH_REQUEST = 0, 1, 3, 4
+CD732_SEARCH_REQUEST, TEST_REQUEST = 5, 7
 
 
 class WireError(RuntimeError):
@@ -71,7 +71,7 @@ class Conn:
 def setup(addr, log_num_files, file_size_bytes, k, r, rho=1, num_threads=1, is_byzantine=0,
           mode=0, t=1, b=0):
     """SETUP_REQUEST with the fields of common.go:51-65 (no MAC): mode 0 tree, 1 multiparty,
-    3 Hollanti."""
+    3 Hollanti, 4 covering design."""
     host, port = addr
     req = {"BenchmarkDir": "", "LogNumFiles": log_num_files, "FileSizeBytes": file_size_bytes,
            "T": t, "K": k, "R": r, "B": b, "Rho": rho, "Mode": mode, "IsByzantine": is_byzantine,
@@ -91,6 +91,13 @@ def multiparty_search(addr, key):
     host, port = addr
     with Conn(host, port) as c:
         return c.call(MULTIPARTY_SEARCH_REQUEST, {"Key": bytes(key)})
+
+
+def cd_search(addr, key):
+    """CD732_SEARCH_REQUEST (server_util/cd732.go:16-100): Results = NUM_CD_KEYS answers."""
+    host, port = addr
+    with Conn(host, port) as c:
+        return c.call(CD732_SEARCH_REQUEST, {"Key": bytes(key)})
 
 
 def hollanti_search(addr, keys):

@@ -22,6 +22,9 @@
  *                                                                 multiparty_dpf.cpp:467-615
  *   pir_engine_mp_key_len            calcMultiPartyOptDPFKeyLength          utils.cpp:105-116
  *   pir_engine_mp_num_keys           NUM_RSS_KEYS                           params.cpp:618
+ *   pir_engine_answer_cd[_dev]       runCDQueryThread (evalAllCDThread)     server.cpp:443-492,
+ *                                                                 multiparty_dpf.cpp:617-690
+ *   pir_engine_cd_key_len            calcCDDPFKeyLength                     utils.cpp:118-129
  *   pir_engine_key_len               calcOptimizedDPFTreeKeyLength          utils.cpp:85-90
  *   pir_comm_* + partitions          (new) split-shard across GPUs, XOR all-reduce over RCCL
  */
@@ -147,6 +150,21 @@ int pir_engine_answer_mp_dev(pir_engine_t *e, const uint8_t *d_key, int p, int t
 int pir_engine_mp_num_keys(int p, int t);
 int pir_engine_mp_key_len(int p, int n, int t);
 long long pir_engine_mp_eval_bytes(int p, int n, int t); /* -1: no layout for (p, n, t) */
+/* Covering-design sqrt(N) DPF answer (runCDQueryThread, server.cpp:443-492): the multiparty
+ * evaluation and scan above on the layout of evalAllCDThread (multiparty_dpf.cpp:617-690):
+ * NUM_CD_KEYS output shares (the engine must have num_rounds == num_cd_keys), 2^(q-1) seeds per
+ * row (q = NUM_CD_KEYS_NEEDED), mu = 2^(n/2 + 3) records per row (integer n / 2), nu = 2^n / mu
+ * rows (0 when mu > 2^n: the answer is zero), the same thread slices.  key_bytes >=
+ * pir_engine_cd_key_len(...) (= the bytes the evaluation reads).  Always the honest answer:
+ * both branches of runCDQueryThread compute it (server.cpp:466-485). */
+int pir_engine_answer_cd(pir_engine_t *e, const uint8_t *key, uint64_t key_bytes,
+                         int num_cd_keys_needed, int num_cd_keys, int thread_num, int num_threads,
+                         uint8_t *result);
+int pir_engine_answer_cd_dev(pir_engine_t *e, const uint8_t *d_key, int num_cd_keys_needed,
+                             int num_cd_keys, int thread_num, int num_threads, uint8_t *d_result,
+                             void *stream);
+/* calcCDDPFKeyLength(p, n, t, q, c) (p and t unused there too); 0 for no layout */
+int pir_engine_cd_key_len(int p, int n, int t, int num_cd_keys_needed, int num_cd_keys);
 /* DPF shares of this engine's rows: out[a*R + i] (dataShare[a][i]) */
 int pir_engine_eval_all(pir_engine_t *e, const uint8_t *key, uint8_t *out);
 

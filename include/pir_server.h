@@ -11,11 +11,13 @@
  *                                      partial answer over rows [t*N/T,(t+1)*N/T); the reference
  *                                      body is defective)
  *   assemblDPFTreeQueryThreadResults   server.h:53,     server.cpp:553-562
- *   setSystemParams / freeParams       params.h:63-64,  params.cpp:467-642 (tree, multiparty and
- *                                      Hollanti modes; the others abort)
+ *   setSystemParams / freeParams       params.h:63-64,  params.cpp:467-642 (tree, multiparty,
+ *                                      Hollanti and covering-design modes; the others abort)
  *   runOptimizedMultiPartyDPFQuery[Thread], assembleMultipartyDPFQueryThreadResults
  *                                      server.h:37,46,52, server.cpp:136-176, :384-441
  *   calcMultiPartyOptDPFKeyLength      utils.h,         utils.cpp:105-116
+ *   runCDQueryThread, assembleCDQueryThreadResults, calcCDDPFKeyLength
+ *                                      server.h:49,53,  server.cpp:443-503, utils.cpp:118-129
  *   runHollantiQuery[Thread], assemble*QueryThreadResults, the other modes' entry points (abort)
  *                                      server.h:39-53,  server.cpp:304-665
  *   encode_within_files_server         client.h:29,     client.cpp:93-110
@@ -30,6 +32,9 @@
  * Deliberate differences (each a reference defect):
  *   - ctx / ctxThreads hold the engine handle instead of OpenSSL contexts (no Go code reads them);
  *   - NUM_RESPONSES is computed after NUM_PARTIES (params.cpp:473 reads it before);
+ *   - every setSystemParams starts from the covering designs' M = 4 and isRss = 1
+ *     (params.cpp:12, :372): the reference keeps the M = 2 of a K = 2, B = 1 CD setup
+ *     (params.cpp:440) and a cleared isRss (:520-599) for all later calls;
  *   - no Woodruff MAPPING_INDEX tables (params.cpp:621-640; out of scope, and overflowing).
  */
 #ifndef PIR_SERVER_H
@@ -80,7 +85,8 @@ extern int MAC_SIZE_BYTES;
 extern int CHECK_MAC;
 /* globals of the other PIR modes (params.h:39-54), read by the Go mode handlers
  * (src/server_util/{multiparty,cd732,woodruff}.go); NUM_RSS_KEYS = the multiparty answer's
- * share count (params.cpp:603-619), the others' modes are not served (see below) */
+ * share count (params.cpp:603-619), NUM_CD_KEYS the covering-design answer's (params.cpp:519-599);
+ * the Shamir and Woodruff modes are not served (see below) */
 extern int NUM_RSS_KEYS;
 extern int NUM_CD_KEYS;
 extern int WOODRUFF_M;
@@ -122,18 +128,25 @@ void runOptimizedMultiPartyDPFQueryThread(server *s, uint8_t *key, int threadNum
 void assembleMultipartyDPFQueryThreadResults(server *s, uint8_t ***in, int numThreads,
                                              uint8_t **out);
 
+/* ---- covering-design sqrt(N) DPF PIR (mode 4, src/server_util/cd732.go:64):
+ *      evalAllCDThread (multiparty_dpf.cpp:617-690) + the GF(2^8) scan on the engine
+ *      (pir_engine_answer_cd).  key = calcCDDPFKeyLength(NUM_PARTIES, LOG_NUM_ENCODED_FILES, T,
+ *      NUM_CD_KEYS_NEEDED, NUM_CD_KEYS) bytes (genCDDPF's layout, multiparty_dpf.cpp:275-408);
+ *      result[a], a < NUM_CD_KEYS, = ENCODED_FILE_SIZE_BYTES over rows
+ *      [threadNum*S*mu, (threadNum+1)*S*mu), S = nu / numThreads (server.cpp:461-485; both
+ *      of its branches are the honest answer). ---- */
+void runCDQueryThread(server *s, uint8_t *key, int threadNum, int numThreads, uint8_t **result);
+void assembleCDQueryThreadResults(server *s, uint8_t ***in, int numThreads, uint8_t **out);
+
 /* ---- the other PIR modes' server entry points, bound by src/server_util/ (shamir.go:52,
- *      cd732.go:64, woodruff.go:69).  Their modes are outside this engine's scope:
- *      setSystemParams refuses modes 2, 4, 5, 6, and these abort with a message if reached
- *      anyway.  The assemble functions are the reference's XOR folds (server.cpp:304-319,
- *      494-503, 647-665). ---- */
+ *      woodruff.go:69).  Their modes are outside this engine's scope: setSystemParams refuses
+ *      modes 2, 5, 6, and these abort with a message if reached anyway.  The assemble functions
+ *      are the reference's XOR folds (server.cpp:304-319, 647-665). ---- */
 void runOptShamirDPFQueryThread(server *s, uint8_t **keys, int threadNum, int startIndex,
                                 int endIndex, uint8_t **result);
-void runCDQueryThread(server *s, uint8_t *key, int threadNum, int numThreads, uint8_t **result);
 void runWoodruffQueryThread(server *s, uint8_t *key, int threadNum, int startIndex, int endIndex,
                             uint8_t **result);
 void assembleShamirQueryThreadResults(server *s, uint8_t ***in, int numThreads, uint8_t **out);
-void assembleCDQueryThreadResults(server *s, uint8_t ***in, int numThreads, uint8_t **out);
 void assembleWoodruffQueryThreadResults(server *s, uint8_t ***in, int numThreads, uint8_t **out);
 /* utils.h:29-30 */
 int calcShamirDPFKeyLength(int log_domainSize);
@@ -164,7 +177,7 @@ void lagrangeInterpolationSemihonest(uint8_t *evalPoints, uint8_t numPoints, uin
 #ifndef SWIG
 typedef unsigned __int128 uint128_t; /* utils.h:13-15 */
 #endif
-extern int NUM_CD_KEYS_NEEDED;       /* params.h:55 (0: covering-design modes are not served) */
+extern int NUM_CD_KEYS_NEEDED;       /* params.h:55 */
 /* client.cpp:144-153 (tree.go:55): finalCW gf_pow(j, RHO*i) ^ 1 and genOptimizedDPF
  * (dpf_tree.cpp:142-274) on the GPU (pir_gen_keys), root seeds from the OS CSPRNG (the
  * reference: RAND_bytes); (*keys)[j] = party j's calcOptimizedDPFTreeKeyLength-byte key. */
@@ -182,8 +195,9 @@ int calcCDDPFKeyLength(int p, int log_domainSize, int t, int num_cd_keys_needed,
                        int num_cd_keys); /* utils.cpp:118-129 */
 int calcWoodruffKeyLength(int p, int r, int t, int logDomainSize,
                           int fileSizeBytes); /* utils.cpp:145-153 */
-/* The other modes' client halves (multiparty key generation and decode, CD, Shamir, Woodruff):
- * their server modes are refused at setSystemParams; these abort with a message. */
+/* The other modes' client halves (multiparty key generation and decode, CD key generation and
+ * decode, Shamir, Woodruff): outside the server path this engine replaces; these abort with a
+ * message. */
 void generateMultiPartyDPFQuery(client *c, int index, uint8_t ***keys);
 void assembleMultiPartyResponses(client *c, uint8_t *erasureIndexList, uint8_t ***responses,
                                  uint8_t *output);

@@ -449,15 +449,16 @@ void orc_mp_sizes(int p, int n, int t, uint64_t *o) {
     o[5] = (uint64_t)(int)(16 * p2 * knu + nrk * knu * p2 + p2 * kmu);
 }
 
-void orc_mp_eval(int p, int n, int t, const uint8_t *key, int thread_num, int num_threads,
-                 uint8_t *out) {
-    uint64_t z[6];
-    orc_mp_sizes(p, n, t, z);
+/* share[a][i*mu + x] over rows [thread_num*slice, (thread_num+1)*slice) of a layout
+   {nrk, p2, mu, nu}: the loop both evalAllOptMultiPartyDPFThread (multiparty_dpf.cpp:590-601)
+   and evalAllCDThread (:665-675) run */
+static void layout_eval(const uint64_t *z, int n, const uint8_t *key, int thread_num,
+                        int num_threads, uint8_t *out) {
     const uint64_t nrk = z[0], p2 = z[1], mu = z[2], nu = z[3], N = 1ull << n;
     const uint64_t tog = nu * 16 * p2, cw = tog + nrk * nu * p2, slice = nu / num_threads;
     uint8_t *g = malloc(mu);
     memset(out, 0, nrk * N);
-    for (uint64_t i = thread_num * slice; i < (thread_num + 1) * slice; i++)   /* :590-601 */
+    for (uint64_t i = thread_num * slice; i < (thread_num + 1) * slice; i++)
         for (uint64_t j = 0; j < p2; j++) {
             orc_G(key + i * 16 * p2 + 16 * j, (uint32_t)mu, g);
             for (uint64_t a = 0; a < nrk; a++) {
@@ -469,17 +470,57 @@ void orc_mp_eval(int p, int n, int t, const uint8_t *key, int thread_num, int nu
     free(g);
 }
 
-void orc_mp_answer(int p, int t, int n, int efs, const uint8_t *key, const uint8_t *shard,
-                   int thread_num, int num_threads, uint8_t *result) {
-    uint64_t z[6];
-    orc_mp_sizes(p, n, t, z);
+/* the scan of runOptimizedMultiPartyDPFQueryThread (server.cpp:416-422) and runCDQueryThread
+   (:477-484) over the thread's slice of rows */
+static void layout_answer(const uint64_t *z, int n, int efs, const uint8_t *key,
+                          const uint8_t *shard, int thread_num, int num_threads, uint8_t *result) {
     const uint64_t nrk = z[0], mu = z[2], nu = z[3], N = 1ull << n, slice = nu / num_threads;
     uint8_t *c = malloc(nrk * N);
-    orc_mp_eval(p, n, t, key, thread_num, num_threads, c);
+    layout_eval(z, n, key, thread_num, num_threads, c);
     memset(result, 0, nrk * efs);
-    for (uint64_t i = thread_num * slice * mu; i < (thread_num + 1) * slice * mu; i++) /* :416-422 */
+    for (uint64_t i = thread_num * slice * mu; i < (thread_num + 1) * slice * mu; i++)
         for (int b = 0; b < efs; b++)
             for (uint64_t a = 0; a < nrk; a++)
                 result[a * efs + b] ^= orc_gf_mul(c[a * N + i], shard[i * (uint64_t)efs + b]);
     free(c);
+}
+
+void orc_mp_eval(int p, int n, int t, const uint8_t *key, int thread_num, int num_threads,
+                 uint8_t *out) {
+    uint64_t z[6];
+    orc_mp_sizes(p, n, t, z);
+    layout_eval(z, n, key, thread_num, num_threads, out);
+}
+
+void orc_mp_answer(int p, int t, int n, int efs, const uint8_t *key, const uint8_t *shard,
+                   int thread_num, int num_threads, uint8_t *result) {
+    uint64_t z[6];
+    orc_mp_sizes(p, n, t, z);
+    layout_answer(z, n, efs, key, shard, thread_num, num_threads, result);
+}
+
+/* ---- covering-design (CD) sqrt(N) DPF ------------------------------------------------------ */
+void orc_cd_sizes(int n, int q_needed, int num_cd_keys, uint64_t *o) {
+    /* evalAllCDThread (multiparty_dpf.cpp:620-625): p2 = 2^(q-1), mu_pow = n/2 + 3 (integer
+       n/2: ceil((double)(n/2))), nu = 2^(n - mu_pow) (0 below 1: (uint64_t)pow(2, negative)) */
+    const int mu_pow = n / 2 + 3;
+    const uint64_t p2 = 1ull << (q_needed - 1), mu = 1ull << mu_pow;
+    const uint64_t nu = mu_pow > n ? 0 : 1ull << (n - mu_pow), nrk = (uint64_t)num_cd_keys;
+    o[0] = nrk; o[1] = p2; o[2] = mu; o[3] = nu;
+    o[4] = 16 * p2 * nu + nrk * nu * p2 + p2 * mu;            /* calcCDDPFKeyLength, utils.cpp:118 */
+    o[5] = (uint64_t)(int)o[4];
+}
+
+void orc_cd_eval(int n, int q_needed, int num_cd_keys, const uint8_t *key, int thread_num,
+                 int num_threads, uint8_t *out) {
+    uint64_t z[6];
+    orc_cd_sizes(n, q_needed, num_cd_keys, z);
+    layout_eval(z, n, key, thread_num, num_threads, out);
+}
+
+void orc_cd_answer(int n, int q_needed, int num_cd_keys, int efs, const uint8_t *key,
+                   const uint8_t *shard, int thread_num, int num_threads, uint8_t *result) {
+    uint64_t z[6];
+    orc_cd_sizes(n, q_needed, num_cd_keys, z);
+    layout_answer(z, n, efs, key, shard, thread_num, num_threads, result);
 }

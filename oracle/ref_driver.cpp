@@ -460,4 +460,88 @@ void ref_mp_server_answer(void* hv, int p, int t, int nrk, const uint8_t* key, i
     assembleMultipartyDPFQueryThreadResults(&h->s, in.data(), num_threads, res.data());
 }
 
+// ---- covering-design (CD) sqrt(N) DPF (mode 4) -----------------------------------------------
+// params.cpp:12 `int M = 4`: setModeParams(CD) sets it to 2 for K = 2, B = 1 and nothing resets
+// it, so every setup below starts from the default (a fresh process would)
+extern int M;
+
+// setSystemParams(L,f,t,k,r,b,rho,0,mode=4) sizing: p, n, efs, NUM_CD_KEYS, NUM_CD_KEYS_NEEDED,
+// calcCDDPFKeyLength (utils.cpp:118-129)
+void ref_cd_sizes(int L, int f, int t, int k, int r, int b, int rho, int* out6) {
+    M = 4;
+    setSystemParams(L, f, t, k, r, b, rho, 0, 4);
+    out6[0] = NUM_PARTIES;
+    out6[1] = LOG_NUM_ENCODED_FILES;
+    out6[2] = ENCODED_FILE_SIZE_BYTES;
+    out6[3] = NUM_CD_KEYS;
+    out6[4] = NUM_CD_KEYS_NEEDED;
+    out6[5] = calcCDDPFKeyLength(NUM_PARTIES, LOG_NUM_ENCODED_FILES, T, NUM_CD_KEYS_NEEDED,
+                                 NUM_CD_KEYS);
+}
+
+// The CD harness of correctness_tests.cpp:568-715 (the reference's one active test, main :1236)
+// with the Go server's encode-across setup: setSystemParams(mode 4), the synthetic DB
+// (client.cpp:16-33), p servers encoded across files (client.cpp:70-97; the last b of them
+// Byzantine, as the harness marks them -- runCDQueryThread answers honestly either way,
+// server.cpp:464-485), generateCDQuery (client.cpp:159-161 -> genCDDPF,
+// multiparty_dpf.cpp:275-408), every party's answer from nthreads runCDQueryThread slices +
+// assembleCDQueryThreadResults (server.cpp:443-503), the first r parties erased,
+// assembleCDResponses (client.cpp:562-615) when `decode`.  Buffers: shards[p*N*efs],
+// keys[p*kl], answers[p*nck*efs], decoded[f].  Returns 1 when decoded == file[idx] (-1: no decode).
+int ref_cd_e2e(int L, int f, int t, int k, int r, int b, int rho, int idx, int nthreads,
+               int decode, uint8_t* shards, uint8_t* keys_out, uint8_t* answers,
+               uint8_t* decoded) {
+    M = 4;
+    setSystemParams(L, f, t, k, r, b, rho, 0, 4);
+    int p = NUM_PARTIES, nck = NUM_CD_KEYS, efs = ENCODED_FILE_SIZE_BYTES;
+    size_t N = NUM_ENCODED_FILES;
+    int kl = calcCDDPFKeyLength(p, LOG_NUM_ENCODED_FILES, T, NUM_CD_KEYS_NEEDED, NUM_CD_KEYS);
+    client c;
+    initialize_client(&c, L, FILE_SIZE_BYTES);
+    std::vector<server> servers(p);
+    for (int i = p - 1, byz = 0; i >= 0; i--) {
+        const int isByz = byz < b ? 1 : 0;
+        byz += isByz;
+        initializeServer(&servers[i], i + 1, LOG_NUM_ENCODED_FILES, efs, isByz, nthreads);
+        encode_across_files_server(&c, &servers[i]);
+        for (size_t j = 0; j < N; j++)
+            memcpy(shards + ((size_t)i * N + j) * efs, servers[i].indexList[j], efs);
+    }
+    uint8_t** keys = (uint8_t**)malloc(p * sizeof(uint8_t*));
+    for (int j = 0; j < p; j++) keys[j] = (uint8_t*)malloc(kl);
+    generateCDQuery(&c, idx, &keys);
+    std::vector<std::vector<uint8_t*>> resp(p, std::vector<uint8_t*>(nck));
+    for (int i = 0; i < p; i++) {
+        memcpy(keys_out + (size_t)i * kl, keys[i], kl);
+        for (int a = 0; a < nck; a++) resp[i][a] = answers + ((size_t)i * nck + a) * efs;
+        std::vector<std::vector<std::vector<uint8_t>>> buf(
+            nthreads, std::vector<std::vector<uint8_t>>(nck, std::vector<uint8_t>(efs)));
+        std::vector<std::vector<uint8_t*>> rows(nthreads, std::vector<uint8_t*>(nck));
+        std::vector<uint8_t**> in(nthreads);
+        for (int th = 0; th < nthreads; th++) {
+            for (int a = 0; a < nck; a++) rows[th][a] = buf[th][a].data();
+            in[th] = rows[th].data();
+            runCDQueryThread(&servers[i], keys[i], th, nthreads, in[th]);
+        }
+        assembleCDQueryThreadResults(&servers[i], in.data(), nthreads, resp[i].data());
+    }
+    int ok = -1;
+    if (decode) {
+    std::vector<uint8_t> erasure(p);
+    for (int i = 0; i < p; i++) erasure[i] = (i < r) ? 0 : 1;
+    uint8_t*** test = (uint8_t***)malloc((p - r) * sizeof(uint8_t**));
+    for (int i = 0, cur = 0; i < p; i++)
+        if (erasure[i]) test[cur++] = resp[i].data();
+    std::vector<uint8_t> out(FILE_SIZE_BYTES);
+    assembleCDResponses(&c, erasure.data(), test, out.data());
+    memcpy(decoded, out.data(), f);
+    ok = memcmp(out.data(), c.unencoded_files[idx], f) == 0;
+    free(test);
+    }
+    for (int j = 0; j < p; j++) free(keys[j]);
+    free(keys);
+    for (int i = 0; i < p; i++) freeServer(&servers[i]);
+    return ok;
+}
+
 }  // extern "C"

@@ -188,3 +188,42 @@ def mp_answer(p, t, n, efs, key, shard, thread_num=0, num_threads=1):
     lib().orc_mp_answer(p, t, n, efs, P(np.ascontiguousarray(key, np.uint8)),
                         P(np.ascontiguousarray(shard, np.uint8)), thread_num, num_threads, P(out))
     return out.reshape(z["nrk"], efs)
+
+
+# ---- covering-design sqrt(N) DPF (mode 4) ----------------------------------------------------
+def cd_sizes(n, q_needed, num_cd_keys):
+    """{nrk, p2, mu, nu, eval_bytes, key_len} of evalAllCDThread (multiparty_dpf.cpp:620-625,
+    utils.cpp:118-129): p2 = 2^(q_needed-1), mu = 2^(n//2+3), nrk = NUM_CD_KEYS."""
+    o = (ctypes.c_uint64 * 6)()
+    lib().orc_cd_sizes(n, q_needed, num_cd_keys, o)
+    return dict(zip(("nrk", "p2", "mu", "nu", "eval_bytes", "key_len"), [int(v) for v in o]))
+
+
+def cd_key(n, q_needed, num_cd_keys, seed):
+    """A synthetic covering-design key (the evaluation is a function of the key bytes; the
+    fixtures of tests/golden/cd.json hold the reference's own genCDDPF keys): xorshift bytes,
+    toggle bytes mapped to {0, 1, the raw byte} as mp_key."""
+    z = cd_sizes(n, q_needed, num_cd_keys)
+    key = xorshift(seed, max(z["eval_bytes"], 16))
+    lo = z["nu"] * 16 * z["p2"]
+    hi = lo + z["nrk"] * z["nu"] * z["p2"]
+    tb = key[lo:hi]
+    key[lo:hi] = np.where(tb % 3 == 0, 0, np.where(tb % 3 == 1, 1, tb))
+    return key
+
+
+def cd_eval(n, q_needed, num_cd_keys, key, thread_num=0, num_threads=1):
+    z = cd_sizes(n, q_needed, num_cd_keys)
+    out = np.zeros(z["nrk"] << n, np.uint8)
+    lib().orc_cd_eval(n, q_needed, num_cd_keys, P(np.ascontiguousarray(key, np.uint8)),
+                      thread_num, num_threads, P(out))
+    return out.reshape(z["nrk"], 1 << n)
+
+
+def cd_answer(n, q_needed, num_cd_keys, efs, key, shard, thread_num=0, num_threads=1):
+    """runCDQueryThread (server.cpp:443-492) on one thread's slice of rows."""
+    z = cd_sizes(n, q_needed, num_cd_keys)
+    out = np.zeros(z["nrk"] * efs, np.uint8)
+    lib().orc_cd_answer(n, q_needed, num_cd_keys, efs, P(np.ascontiguousarray(key, np.uint8)),
+                        P(np.ascontiguousarray(shard, np.uint8)), thread_num, num_threads, P(out))
+    return out.reshape(z["nrk"], efs)

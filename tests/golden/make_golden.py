@@ -374,12 +374,53 @@ def mp():
     write("multiparty.json", {"cases": cases, "setup_sizes": sizes})
 
 
+CD_CASES = [  # (L, f, t, k, r, b, rho, index, threads, decode): P = 8 (CD842, the reference's
+    # own runCDPirTests setup, correctness_tests.cpp:1236), 16 (CD1682), 14 (CD1472), 12 (CD1262).
+    # genCDDPF puts index a at row gamma = a >> (n/2), column delta = a mod 2^(n/2)
+    # (multiparty_dpf.cpp:283-284) and reads s[gamma] of nu = 2^(n - n/2 - 3) rows: an index with
+    # gamma >= nu reads past its seed array, so the indices below keep gamma < nu (gamma > 0 in
+    # the last three, decode off: their point is record gamma*mu + delta, not a)
+    (15, 8, 2, 2, 0, 1, 1, 1, 4, 1), (12, 64, 2, 4, 0, 2, 1, 3 * 32 + 5, 2, 0),
+    (13, 40, 2, 3, 1, 2, 1, 6 * 64 + 9, 8, 0), (11, 33, 2, 4, 0, 1, 1, 2 * 16 + 3, 1, 0)]
+
+
+def cd():
+    """Covering-design sqrt(N) DPF PIR (mode 4): the reference's own CD harness with its own key
+    generation (generateCDQuery -> genCDDPF), encode-across shards, every party's answer from
+    runCDQueryThread slices + assembleCDQueryThreadResults, and the decode.  Keys are kept for
+    three parties per case (first, middle, last) to bound the fixture's size."""
+    REF.ref_cd_sizes.restype = None
+    cases = []
+    for (L, f, t, k, r, b, rho, idx, T, dec_ok) in CD_CASES:
+        s = (ctypes.c_int * 6)()
+        REF.ref_cd_sizes(L, f, t, k, r, b, rho, s)
+        p, n, efs, nck, qn, kl = list(s)
+        N = 1 << n
+        shards = np.zeros(p * N * efs, np.uint8)
+        keys = np.zeros(p * kl, np.uint8)
+        ans = np.zeros(p * nck * efs, np.uint8)
+        dec = np.zeros(f, np.uint8)
+        ok = REF.ref_cd_e2e(L, f, t, k, r, b, rho, idx, T, int(dec_ok), ptr(shards), ptr(keys), ptr(ans), ptr(dec))
+        kept = sorted({0, p // 2, p - 1})
+        cases.append({
+            "L": L, "f": f, "t": t, "k": k, "r": r, "b": b, "rho": rho, "index": idx, "threads": T,
+            "p": p, "n": n, "efs": efs, "num_cd_keys": nck, "num_cd_keys_needed": qn,
+            "key_len": kl, "decoded_ok": int(ok),  # -1: decode not run
+            "shard_sha256": [sha(shards[i * N * efs:(i + 1) * N * efs]) for i in range(p)],
+            "key_sha256": [sha(keys[i * kl:(i + 1) * kl]) for i in range(p)],
+            "keys": {str(i + 1): keys[i * kl:(i + 1) * kl].tobytes().hex() for i in kept},
+            "answers": [ans[i * nck * efs:(i + 1) * nck * efs].tobytes().hex() for i in range(p)],
+        })
+        print("cd case", L, f, t, k, r, b, "p", p, "n", n, "keys", nck, "/", qn, "kl", kl, "ok", ok)
+    write("cd.json", {"cases": cases})
+
+
 if __name__ == "__main__":
     REF.ref_server_new.restype = ctypes.c_void_p
     REF.ref_blen.restype = ctypes.c_uint32
     for fn in (REF.ref_gf_mul, REF.ref_gf_pow, REF.ref_gf_inv):
         fn.restype = ctypes.c_uint8
-    what = sys.argv[1:] or ["prg", "gf", "dpf", "e2e", "thread", "fullsize", "hollanti", "mp", "client"]
+    what = sys.argv[1:] or ["prg", "gf", "dpf", "e2e", "thread", "fullsize", "hollanti", "mp", "client", "cd"]
     if "prg" in what: prg_kats()
     if "gf" in what: gf_kats()
     if "dpf" in what: dpf_and_answers()
@@ -390,3 +431,4 @@ if __name__ == "__main__":
     if "client" in what: client_kats()
     if "hollanti" in what: hollanti()
     if "mp" in what: mp()
+    if "cd" in what: cd()

@@ -24,9 +24,9 @@ def _free_port():
 
 
 class Servers:
-    def __init__(self, p, byzantine=()):
+    def __init__(self, p, byzantine=(), parties=None):
         self.procs, self.addrs = [], []
-        for party in range(1, p + 1):
+        for party in parties or range(1, p + 1):
             port = _free_port()
             args = [SERVE, "--port", str(port), "--party", str(party)]
             if party in byzantine:
@@ -163,3 +163,23 @@ def test_hollanti_over_the_wire(serve_bin):
         resp = wire.hollanti_search(sv.addrs[1], keys)
     got = np.stack([np.frombuffer(b, np.uint8) for b in resp["Results"]])
     assert np.array_equal(got, O.scan(keys, shard, efs))
+
+
+@pytest.mark.gpu
+def test_cd_over_the_wire(serve_bin):
+    """Mode 4 (covering-design sqrt(N) DPF): three servers (parties 1, 5, 8 of the reference's
+    own P = 8 CD842 setup, correctness_tests.cpp:1236) set up over the wire encode across files
+    on the GPU; their CD732_SEARCH answers to the reference's genCDDPF keys == the reference's
+    answers (tests/golden/cd.json)."""
+    import _oracle as O
+    c = O.golden("cd.json")["cases"][0]
+    parties = sorted(map(int, c["keys"]))
+    with Servers(len(parties), parties=parties) as sv:
+        for addr in sv.addrs:
+            wire.setup(addr, c["L"], c["f"], c["k"], c["r"], c["rho"], mode=4, t=c["t"], b=c["b"])
+        resps = [wire.cd_search(addr, bytes.fromhex(c["keys"][str(q)]))
+                 for addr, q in zip(sv.addrs, parties)]
+        with pytest.raises(wire.WireError):
+            wire.multiparty_search(sv.addrs[0], b"\0" * 64)
+    for q, resp in zip(parties, resps):
+        assert b"".join(resp["Results"]).hex() == c["answers"][q - 1], q
