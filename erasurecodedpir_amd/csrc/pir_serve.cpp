@@ -285,9 +285,11 @@ std::string setup(const MVal& req) {  // server.go:295-331
     return "answer rows outside [1,16] (NUM_ROUNDS / NUM_RSS_KEYS / NUM_CD_KEYS)";
   pir_engine_config c{};
   c.device = g.device;
-  // the party count only sizes tree-DPF keys (modes 1, 3 and 4 answer other key forms)
-  c.num_parties = mode == 0 ? NUM_PARTIES : 2;
-  c.party_index = mode == 0 ? g.party : 1;
+  // the party count only sizes tree-DPF keys (modes 1, 3 and 4 answer other key forms); the
+  // party index also selects the encode-across evaluation point gf_pow(party, j) (client.cpp:
+  // 84-89), so the encode-across modes keep the server's own (Hollanti passes it explicitly)
+  c.num_parties = mode == 3 ? 2 : (NUM_PARTIES < 2 ? 2 : NUM_PARTIES);
+  c.party_index = mode == 3 ? 1 : g.party;
   c.log_num_records = LOG_NUM_ENCODED_FILES;
   c.record_bytes = (uint32_t)ENCODED_FILE_SIZE_BYTES;
   c.num_rounds = rounds;

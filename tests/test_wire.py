@@ -122,23 +122,27 @@ def test_erasure_coded_servers_with_one_down(serve_bin):
 
 @pytest.mark.gpu
 def test_multiparty_over_the_wire(serve_bin):
-    """Mode 1 (multiparty sqrt(N) DPF): SETUP encodes across files on the GPU, a
-    MULTIPARTY_SEARCH answer == the CPU restatement on the same encoded shard; a tree request to
-    a multiparty setup is refused with an error."""
+    """Mode 1 (multiparty sqrt(N) DPF): SETUP encodes across files on the GPU (k = 2, so each
+    server's own evaluation point matters: parties 1 and 3), each MULTIPARTY_SEARCH answer ==
+    the CPU restatement on that party's encoded shard; a tree request to a multiparty setup is
+    refused with an error."""
     import _oracle as O
-    L, f, t, k, r = 12, 64, 1, 1, 1
+    L, f, t, k, r = 12, 64, 1, 2, 1
     p = t + k + r
-    key = O.mp_key(p, L, t, 31337)
+    key = O.mp_key(p, L - 1, t, 31337)  # k = 2: the domain is the 2^(L-1) encoded rows
     files = O.synthetic_db(L, f)
-    with Servers(1) as sv:
-        wire.setup(sv.addrs[0], L, f, k, r, mode=1, t=t)
-        resp = wire.multiparty_search(sv.addrs[0], key)
+    with Servers(2, parties=(1, 3)) as sv:  # party 3: its own encode-across evaluation point
+        for addr in sv.addrs:
+            wire.setup(addr, L, f, k, r, mode=1, t=t)
+        resps = [wire.multiparty_search(addr, key) for addr in sv.addrs]
         with pytest.raises(wire.WireError):
             wire.tree_search(sv.addrs[0], b"\0" * 64)
-    got = np.stack([np.frombuffer(b, np.uint8) for b in resp["Results"]])
-    shard = O.encode_across(L, f, k, p, 1, files)
-    assert np.array_equal(got, O.mp_answer(p, t, L, f, key, shard))
-    assert "PartyIndex" not in resp and resp["ServerLatency"] >= 0
+    n = L - 1  # k = 2: 2^(L-1) encoded rows
+    for party, resp in zip((1, 3), resps):
+        got = np.stack([np.frombuffer(b, np.uint8) for b in resp["Results"]])
+        shard = O.encode_across(L, f, k, p, party, files)
+        assert np.array_equal(got, O.mp_answer(p, t, n, f, key, shard)), party
+        assert "PartyIndex" not in resp and resp["ServerLatency"] >= 0
 
 
 @pytest.mark.gpu
