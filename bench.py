@@ -278,10 +278,12 @@ class Ctx:
         self.torch, self.dist = torch, dist
         self.world, self.rank, self.local = world, rank, local
         self.rehearsal = False
+        self.host_fold = False  # no RCCL communicator: partition answers XORed over gloo
 
     def fold(self, arr):
-        """Rehearsal runs only: XOR of every rank's partition answer (gloo all-gather)."""
-        if not self.rehearsal:
+        """Host-fold runs only (rehearsal, or the RCCL-init fallback): XOR of every rank's
+        partition answer (gloo all-gather)."""
+        if not self.host_fold:
             return arr
         t = self.torch.from_numpy(np.ascontiguousarray(arr))
         parts = [self.torch.empty_like(t) for _ in range(self.world)]
@@ -336,18 +338,36 @@ def measure(ctx, eng, keys, W, K, single=True):
     eng.reserve_queue(max(W, K, 1))  # queue buffers sized at setup, as a server would
     if W:
         eng.answer_stream_dev(d_keys, W, d_res)
+    box = {}
+    if ctx.host_fold:
+        # no device exchange: the answers go to the host and are XORed over gloo INSIDE the
+        # timed region (the exchange a split-shard query cannot skip)
+        def run_queue():
+            eng.answer_stream_dev(d_kq, K, d_rq)
+            box["q"] = ctx.fold(eng.d2h(d_rq, ab * K))
+    else:
+        def run_queue():
+            eng.answer_stream_dev(d_kq, K, d_rq)
     eng.set_profiling(1)
-    dt = ctx.timed(eng, lambda: eng.answer_stream_dev(d_kq, K, d_rq))
+    dt = ctx.timed(eng, run_queue)
     phases = eng.last_timings()
     eng.set_profiling(0)
-    queue = eng.d2h(d_rq, ab * K).reshape(K, eng.num_rounds, eng.record_bytes)
+    queue = (box["q"] if ctx.host_fold else eng.d2h(d_rq, ab * K)).reshape(
+        K, eng.num_rounds, eng.record_bytes)
     out = {"ms": dt / K * 1e3, "phases": phases, "answers": queue}
     if single:
         for i in range(max(1, min(W, 5))):  # warm the one-query kernel (its own code object)
             eng.answer_dev(d_keys + (i % nkeys) * kl, d_res + (i % nkeys) * ab)
-        dt1 = ctx.timed(eng, lambda: [eng.answer_dev(d_kq + i * kl, d_rq + i * ab)
-                                      for i in range(K)])
-        singles = eng.d2h(d_rq, ab * K).reshape(K, eng.num_rounds, eng.record_bytes)
+        if ctx.host_fold:
+            def run_singles():
+                box["s"] = [ctx.fold(eng.answer_dev(d_kq + i * kl, d_rq + i * ab) or
+                                     eng.d2h(d_rq + i * ab, ab)) for i in range(K)]
+            dt1 = ctx.timed(eng, run_singles)
+            singles = np.stack(box["s"]).reshape(K, eng.num_rounds, eng.record_bytes)
+        else:
+            dt1 = ctx.timed(eng, lambda: [eng.answer_dev(d_kq + i * kl, d_rq + i * ab)
+                                          for i in range(K)])
+            singles = eng.d2h(d_rq, ab * K).reshape(K, eng.num_rounds, eng.record_bytes)
         eng.set_profiling(max(K, 1))
         for i in range(K):
             eng.answer_dev(d_kq + i * kl, d_rq + i * ab)
@@ -510,13 +530,13 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
     # PIR_BENCH_REHEARSAL=1 (diagnostics, N > 1 on a box with fewer GPUs): ranks share the
     # visible GPUs, no RCCL communicator is attached, and the partition answers are XOR-folded
-    # over gloo on the host for the parity checks (the timed region then holds no exchange)
+    # over gloo on the host inside the timed region (the host-fold exchange below)
     rehearsal = world > 1 and os.environ.get("PIR_BENCH_REHEARSAL") == "1"
     if rehearsal:
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     ctx = Ctx(world, rank, local)
-    ctx.rehearsal = rehearsal
+    ctx.rehearsal = ctx.host_fold = rehearsal
 
     import erasurecodedpir_amd as pir
     from erasurecodedpir_amd.dist import broadcast_bytes, log2_exact
@@ -539,11 +559,11 @@ def main():
 
     eng = pir.Engine(p, 1, n, efs, nq, device=local, log_num_partitions=g, partition_index=rank)
     eng.fill_shard_random(SHARD_SEED)
+    comm_err = None
     if world > 1 and not rehearsal:
-        attach_or_exit(pir, eng, world, rank)
+        comm_err = attach_or_fallback(pir, eng, world, rank)
+        ctx.host_fold = comm_err is not None
     m = measure(ctx, eng, [ks[0] for _, ks in keyset], W, K, single=not args.queue_only)
-    if rehearsal and not args.queue_only:
-        m["answers"], m["singles"] = ctx.fold(m["answers"]), ctx.fold(m["singles"])
     ms = m["ms"]
     shard_bytes = float(1 << n) * efs  # logical shard (all ranks)
     value = shard_bytes / GIB / (ms / 1e3)
@@ -599,8 +619,10 @@ def main():
             f"split shard, weak scaling: {world} x 2^{n_cfg} x {efs} B partitions of one 2^{n} x {efs} B logical shard (RCCL all-gather + XOR fold)",
             "records": 1 << n, "record_bytes": efs, "parties": p, "num_rounds": nq,
             "records_per_gpu": int(eng.num_rows), "dpf_depth": n,
-            "parallelism": (f"split-shard x{world}" + (" (REHEARSAL: shared GPU, no RCCL, "
-                            "host gloo fold outside the timed region)" if rehearsal else ""))
+            "parallelism": (f"split-shard x{world}" + (
+                " (REHEARSAL: shared GPU, no RCCL, host gloo fold inside the timed region)"
+                if rehearsal else (" (host gloo exchange inside the timed region: RCCL "
+                                   "communicator init failed)" if comm_err else "")))
                            if world > 1 else "single",
             "step": "one PIR query: its own DPF key and tree, one full pass over the shard",
             "mode": "query queue: the K timed queries (distinct keys) are answered back to back "
@@ -628,6 +650,9 @@ def main():
         allr = [None] * world
         dist.all_gather_object(allr, mine)
         out["per_rank"] = allr
+        out["exchange"] = ("rccl all-gather + k_xor_fold" if not ctx.host_fold else
+                           "host: D2H + gloo all-gather + numpy XOR" +
+                           (f" (RCCL init failed: {comm_err})" if comm_err else " (rehearsal)"))
     cpu_path = None
     threads_leg = rank == 0 and world == 1 and not args.no_extras and config == "c24"
     if rank == 0 and world == 1 and (not args.no_cpu or threads_leg):
@@ -693,11 +718,14 @@ def main():
         dist.destroy_process_group()
 
 
-def attach_or_exit(pir, eng, world, rank):
-    """Attach the RCCL communicator on every rank, or fail fast: the engine's init is
+def attach_or_fallback(pir, eng, world, rank):
+    """Attach the RCCL communicator on every rank, or fall back together: the engine's init is
     non-blocking and bounded ($PIR_COMM_INIT_TIMEOUT, pir_comm_attach), every rank reports its
-    outcome over gloo, and if any rank failed ALL ranks exit with status 3 and a message
-    (no retry, no re-exec)."""
+    outcome over gloo, and if any rank failed every rank detaches (an engine without a
+    communicator answers its partition) and the run exchanges the partial answers over gloo on
+    the host inside the timed region, labelled in the line -- returns the error, or None.
+    $PIR_BENCH_NO_FALLBACK=1: all ranks exit with status 3 and the message instead (no retry,
+    no re-exec)."""
     import torch.distributed as dist
     from erasurecodedpir_amd.dist import broadcast_bytes
 
@@ -718,13 +746,19 @@ def attach_or_exit(pir, eng, world, rank):
     errs = [None] * world
     dist.all_gather_object(errs, err)
     bad = [(r, e) for r, e in enumerate(errs) if e]
-    if bad:
-        if rank == 0:
-            print(f"bench.py: RCCL communicator init failed on {len(bad)} of {world} ranks: "
-                  + "; ".join(f"rank {r}: {e}" for r, e in bad), file=sys.stderr, flush=True)
+    if not bad:
+        return None
+    msg = (f"RCCL communicator init failed on {len(bad)} of {world} ranks: "
+           + "; ".join(f"rank {r}: {e}" for r, e in bad))
+    if rank == 0:
+        print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+    if os.environ.get("PIR_BENCH_NO_FALLBACK") == "1":
         eng.close()
         dist.destroy_process_group()
         sys.exit(3)
+    if err is None:
+        eng.detach_comm()  # this rank joined a communicator the others did not
+    return msg[:300]
 
 
 def extra_leg(ctx, pir, config, W, K, rng, single=True):

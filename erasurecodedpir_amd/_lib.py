@@ -113,6 +113,7 @@ PROTOTYPES = {
     "pir_engine_trace_query": (_I, [_P, _P, _I, _P, _I]),
     "pir_comm_unique_id": (_I, [_P]),
     "pir_comm_attach": (_I, [_P, _P, _I, _I]),
+    "pir_comm_detach": (_I, [_P]),
     # pir_client.h
     "pir_gen_keys": (_I, [_I, _I, _U64, _P, _I, _I, _P, _P]),
     "pir_final_cw": (None, [_I, _I, _I, _P]),

@@ -204,6 +204,90 @@ __device__ __forceinline__ void aes_ctr_row(const Tab& T, uint4 key, uint4 (&out
   }
 }
 
+// NK independent keys in lockstep, row shape, NB CTR blocks each (counters 0..NB-1): every
+// round of the NK instances is issued together, so a lane keeps NK dependent AES chains in
+// flight.  For levels that are bound by AES latency rather than by LDS lookups (the tree waves
+// of k_query beside the scan: 8 waves, so one chain per lane leaves the LDS mostly idle).
+// Same outputs as NK calls of aes_ctr_row<NB, LASTW, LASTB>(T, key[k], out[k]).
+template <int NK, int NB, int LASTW, int LASTB = 0>
+__device__ __forceinline__ void aes_ctr_rowk(const Tab& T, const uint4 (&key)[NK],
+                                             uint4 (&out)[NK][NB]) {
+  static_assert(LASTB == 0 || (NB == 1 && LASTB < 4), "byte-trimmed: one block, 1-3 bytes");
+  uint32_t k0[NK], k1[NK], k2[NK], k3[NK];
+  uint32_t w[NK][NB][4];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    k0[k] = key[k].x; k1[k] = key[k].y; k2[k] = key[k].z; k3[k] = key[k].w;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      w[k][b][0] = k0[k]; w[k][b][1] = k1[k]; w[k][b][2] = k2[k];
+      w[k][b][3] = k3[k] ^ ((uint32_t)b << 24);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      key_next(T, k0[k], k1[k], k2[k], k3[k], kRcon[r]);
+      const uint32_t r0 = rotr8(k0[k]), r1 = rotr8(k1[k]), r2 = rotr8(k2[k]), r3 = rotr8(k3[k]);
+      auto& wk = w[k];
+      if (r == 0) {  // as aes_ctr_row: the blocks share columns 1-3 after the first round
+#pragma unroll
+        for (int b = 1; b < NB; ++b)
+          wk[b][0] = xor3(T.t0<0>(wk[b][0]), T.t2<2>(wk[b][2]),
+                          rotl8(xor3(T.t0<1>(wk[b][1]), T.t2<3>(wk[b][3]), r0)));
+        round_row(T, wk[0][0], wk[0][1], wk[0][2], wk[0][3], r0, r1, r2, r3);
+#pragma unroll
+        for (int b = 1; b < NB; ++b) {
+          wk[b][1] = wk[0][1]; wk[b][2] = wk[0][2]; wk[b][3] = wk[0][3];
+        }
+      } else if (r == 1) {
+        const uint32_t a1 = wk[0][1], a2 = wk[0][2], a3 = wk[0][3];
+        const uint32_t s0 = T.t2<2>(a2) ^ rotl8(xor3(T.t0<1>(a1), T.t2<3>(a3), r0));
+        const uint32_t s1 = xor3(T.t0<0>(a1), T.t2<2>(a3), rotl8(T.t0<1>(a2) ^ r1));
+        const uint32_t s2 = T.t0<0>(a2) ^ rotl8(xor3(T.t0<1>(a3), T.t2<3>(a1), r2));
+        const uint32_t s3 = xor3(T.t0<0>(a3), T.t2<2>(a1), rotl8(T.t2<3>(a2) ^ r3));
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const uint32_t x = wk[b][0];
+          wk[b][0] = T.t0<0>(x) ^ s0;
+          wk[b][1] = s1 ^ rotl8(T.t2<3>(x));
+          wk[b][2] = s2 ^ T.t2<2>(x);
+          wk[b][3] = s3 ^ rotl8(T.t0<1>(x));
+        }
+      } else {
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          round_row(T, wk[b][0], wk[b][1], wk[b][2], wk[b][3], r0, r1, r2, r3);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    if constexpr (LASTB > 0) {
+      uint32_t t = T.t2<1>(k3[k]);
+      if constexpr (LASTB >= 2) t = (t & 0xffu) | (T.t0<2>(k3[k]) & 0xff00u);
+      if constexpr (LASTB >= 3) t |= T.t0<3>(k3[k]) & 0xff0000u;
+      out[k][0] = make_uint4(
+          last_col_b<LASTB>(T, w[k][0][0], w[k][0][1], w[k][0][2], k0[k] ^ t ^ kRcon[9]), 0, 0, 0);
+    } else {
+      key_next(T, k0[k], k1[k], k2[k], k3[k], kRcon[9]);
+      const uint32_t kk[4] = {k0[k], k1[k], k2[k], k3[k]};
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        uint32_t o[4] = {0, 0, 0, 0};
+        const int nw = (b == NB - 1) ? LASTW : 4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c < nw)
+            o[c] = last_col(T, w[k][b][c], w[k][b][(c + 1) & 3], w[k][b][(c + 2) & 3],
+                            w[k][b][(c + 3) & 3], kk[c]);
+        out[k][b] = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  }
+}
+
 // Row shape, one block with counter `ctr` (generic helper, e.g. key generation).
 __device__ __forceinline__ uint4 aes_ctr_block(const Tab& T, uint4 key, uint32_t ctr) {
   uint32_t k0 = key.x, k1 = key.y, k2 = key.z, k3 = key.w;

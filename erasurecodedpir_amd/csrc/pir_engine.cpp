@@ -1588,6 +1588,20 @@ int pir_comm_unique_id(uint8_t id[PIR_COMM_ID_BYTES]) {
   return PIR_OK;
 }
 
+int pir_comm_detach(pir_engine_t* e) {
+  if (!e) return fail(PIR_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  // abort, not destroy: a peer that never joined (or already left) cannot block the caller
+  if (e->comm) (void)ncclCommAbort(e->comm);
+  e->comm = nullptr;
+  e->comm_failed = false;
+  e->nranks = 1;
+  e->rank = 0;
+  return PIR_OK;
+}
+
 int pir_comm_attach(pir_engine_t* e, const uint8_t id[PIR_COMM_ID_BYTES], int nranks, int rank) {
   if (!e || !id) return fail(PIR_EINVAL, "null argument");
   if (nranks != (1 << e->cfg.log_num_partitions) || rank != e->cfg.partition_index)
@@ -1618,6 +1632,8 @@ int pir_comm_attach(pir_engine_t* e, const uint8_t id[PIR_COMM_ID_BYTES], int nr
   e->comm_failed = false;
   const char* xt = getenv("PIR_COMM_TIMEOUT");  // seconds one exchange may take to enqueue
   if (xt && atof(xt) > 0) e->comm_timeout_s = atof(xt);
+  if (e->d_gather) (void)hipFree(e->d_gather);  // a re-attach (after pir_comm_detach)
+  e->d_gather = nullptr;
   HIP_TRY(hipMalloc(&e->d_gather, (size_t)nranks * e->cfg.num_rounds * e->cfg.record_bytes));
   return PIR_OK;
 }

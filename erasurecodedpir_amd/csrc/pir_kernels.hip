@@ -1175,6 +1175,12 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
 // Scan waves are k_fused's; at the end of a query they fold their bit planes into LDS and
 // write the workgroup's partial answer (slab) of that query.
 // ------------------------------------------------------------------------------------------
+// k_query tree waves: nodes per lane in flight on the wide row-shape levels and the leaf level
+// (1 = one AES chain per lane, the round-3 form; PIR_TREE_ILP at build time)
+#ifndef PIR_TREE_ILP
+#define PIR_TREE_ILP 1
+#endif
+constexpr int kTreeIlp = PIR_TREE_ILP;
 constexpr int kQueryCwCap = 256;  // (levels x (p-1)) correction words staged in LDS
 constexpr int kQueryKin = 6;      // a tile's input nodes sit 6 levels below its root (64 of them)
 
@@ -1372,6 +1378,33 @@ __global__ __launch_bounds__(NT) void k_query(
               ot[2 * u + 1] = (tb >> B.pm1) & B.tmask;
             }
           }
+        } else if (kTreeIlp > 1 && W >= 2 * nt) {
+          // row shape, two nodes per lane with their AES rounds interleaved: the tree waves
+          // beside the scan are few, so one dependent AES chain per lane leaves the LDS idle
+          // (the second node of a lane past W repeats the first and stores nothing)
+          for (int u0 = tt; u0 < W; u0 += 2 * nt) {
+            const bool ok1 = u0 + nt < W;
+            const int uu[2] = {u0, ok1 ? u0 + nt : u0};
+            uint4 cs[2], key[2];
+            uint32_t ct[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              cw(L, it[uu[k]], cs[k], ct[k]);
+              key[k] = is[uu[k]];
+            }
+            uint4 o[2][3];
+            aes_ctr_rowk<2, 3, 1>(T, key, o);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              if (k == 1 && !ok1) break;
+              const int u = uu[k];
+              const uint32_t tb = (o[k][2].x & B.tb_mask) ^ ct[k];
+              os[2 * u] = xor4(o[k][0], cs[k]);
+              os[2 * u + 1] = xor4(o[k][1], cs[k]);
+              ot[2 * u] = tb & B.tmask;
+              ot[2 * u + 1] = (tb >> B.pm1) & B.tmask;
+            }
+          }
         } else {  // row shape: one lane per node, 3 CTR blocks on one key schedule
           for (int u = tt; u < W; u += nt) {
             uint4 cs;
@@ -1510,6 +1543,53 @@ __global__ __launch_bounds__(NT) void k_query(
             uint4 v = aes_ctr_block(T, xor4(o, cs), 0u);
             for (uint32_t j = 0; j < pm1; ++j) v = xor4(v, and4(sm.lastcw[j], 0u - ((tc >> j) & 1u)));
             store_leaf<NRP>(ring, 2 * u + r, make_uint4(v.x & qm.x, v.y & qm.y, v.z & qm.z, v.w & qm.w));
+          }
+        }
+      } else if (kTreeIlp > 1 && W >= 2 * nt) {
+        // two parents per lane, their AES rounds interleaved, then their four leaf blocks
+        constexpr int NW = NRP <= 4 ? 1 : NRP / 4;
+        for (int u0 = tt; u0 < W; u0 += 2 * nt) {
+          const bool ok1 = u0 + nt < W;
+          const int uu[2] = {u0, ok1 ? u0 + nt : u0};
+          uint4 cs[2], key[2];
+          uint32_t ct[2];
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            cw(L_leaf_parent, it[uu[k]], cs[k], ct[k]);
+            key[k] = is[uu[k]];
+          }
+          uint4 o[2][3];
+          aes_ctr_rowk<2, 3, 1>(T, key, o);
+          uint4 lk[4];
+          uint32_t tc[4];
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const uint32_t tb = (o[k][2].x & B.tb_mask) ^ ct[k];
+            tc[2 * k] = tb & B.tmask;
+            tc[2 * k + 1] = (tb >> B.pm1) & B.tmask;
+            lk[2 * k] = xor4(o[k][0], cs[k]);
+            lk[2 * k + 1] = xor4(o[k][1], cs[k]);
+          }
+          uint4 v[4][1];
+          aes_ctr_rowk<4, 1, NW, (NRP < 4 ? NRP : 0)>(T, lk, v);
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            for (uint32_t j = 0; j < pm1; ++j)
+              v[c][0] = xor4(v[c][0], and4(sm.lastcw[j], 0u - ((tc[c] >> j) & 1u)));
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            if (k == 1 && !ok1) break;
+            const int u = uu[k];
+            const uint4 a = make_uint4(v[2 * k][0].x & qm.x, v[2 * k][0].y & qm.y,
+                                       v[2 * k][0].z & qm.z, v[2 * k][0].w & qm.w);
+            const uint4 c = make_uint4(v[2 * k + 1][0].x & qm.x, v[2 * k + 1][0].y & qm.y,
+                                       v[2 * k + 1][0].z & qm.z, v[2 * k + 1][0].w & qm.w);
+            if constexpr (NRP == 1) {
+              *reinterpret_cast<uint16_t*>(ring + 2 * u) = (uint16_t)((a.x & 0xffu) | ((c.x & 0xffu) << 8));
+            } else {
+              store_leaf<NRP>(ring, 2 * u, a);
+              store_leaf<NRP>(ring, 2 * u + 1, c);
+            }
           }
         }
       } else {

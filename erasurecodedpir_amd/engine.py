@@ -370,6 +370,10 @@ class Engine:
         uid, up = _buf(unique_id)
         check(self._lib.pir_comm_attach(self._h, up, nranks, rank), "pir_comm_attach")
 
+    def detach_comm(self):
+        """Drop the communicator (aborted): this engine answers its partition alone again."""
+        check(self._lib.pir_comm_detach(self._h), "pir_comm_detach")
+
 
 def mp_num_keys(p, t):
     """NUM_RSS_KEYS = choose(p, t) * (p - t) / p (params.cpp:618): shares per multiparty key."""

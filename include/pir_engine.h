@@ -239,6 +239,10 @@ int pir_comm_unique_id(uint8_t id[PIR_COMM_ID_BYTES]);
  * enqueue within $PIR_COMM_TIMEOUT seconds (default 60) aborts the communicator; the engine
  * then refuses every later answer with PIR_ECOMM. */
 int pir_comm_attach(pir_engine_t *e, const uint8_t id[PIR_COMM_ID_BYTES], int nranks, int rank);
+/* drop the communicator (aborted, never waited on) and answer this partition alone again; also
+ * clears the refusal state after a failed exchange.  For callers that fall back to exchanging
+ * partition answers themselves when a communicator could not be set up on every rank. */
+int pir_comm_detach(pir_engine_t *e);
 /* the combine step after the all-gather, on its own: d_gathered = nranks blocks of
  * bytes_per_rank (rank r's partial answers at r * bytes_per_rank: ncclAllGather's output
  * layout); d_result[i] = XOR over r of d_gathered[r * bytes_per_rank + i] (the XOR assembly of
