@@ -1522,7 +1522,10 @@ __global__ __launch_bounds__(NT) void k_query(
     {
       const uint4* is = buf ? sm.sb : sm.sa;
       const uint32_t* it = buf ? sm.tb : sm.ta;
-      if (team == (uint32_t)NWV) {  // 3 lanes per parent; the child lanes convert
+      if (team == (uint32_t)NWV && !(kTreeIlp > 1 && W <= 2 * nt)) {
+        // 3 lanes per parent; the child lanes convert (with kTreeIlp > 1 only for levels wider
+        // than two parents per lane: a narrower last level takes the row shape below, one or
+        // two parents per lane with their leaves' AES interleaved)
         const int l = tt & 63, ul = l / 3, r = l - 3 * ul;
         const int npp = (nt >> 6) * 21;
         const int u0 = (tt >> 6) * 21 + ul;
@@ -1603,8 +1606,16 @@ __global__ __launch_bounds__(NT) void k_query(
           const uint32_t tb = (o[2].x & B.tb_mask) ^ ct;
           const uint32_t tl = tb & B.tmask, tr = (tb >> B.pm1) & B.tmask;
           uint4 vl[1], vr[1];
-          aes_ctr_row<1, NW, (NRP < 4 ? NRP : 0)>(T, xor4(o[0], cs), vl);
-          aes_ctr_row<1, NW, (NRP < 4 ? NRP : 0)>(T, xor4(o[1], cs), vr);
+          if constexpr (kTreeIlp > 1) {  // the two leaf blocks' rounds interleaved
+            const uint4 lk[2] = {xor4(o[0], cs), xor4(o[1], cs)};
+            uint4 v2[2][1];
+            aes_ctr_rowk<2, 1, NW, (NRP < 4 ? NRP : 0)>(T, lk, v2);
+            vl[0] = v2[0][0];
+            vr[0] = v2[1][0];
+          } else {
+            aes_ctr_row<1, NW, (NRP < 4 ? NRP : 0)>(T, xor4(o[0], cs), vl);
+            aes_ctr_row<1, NW, (NRP < 4 ? NRP : 0)>(T, xor4(o[1], cs), vr);
+          }
           for (uint32_t j = 0; j < pm1; ++j) {
             vl[0] = xor4(vl[0], and4(sm.lastcw[j], 0u - ((tl >> j) & 1u)));
             vr[0] = xor4(vr[0], and4(sm.lastcw[j], 0u - ((tr >> j) & 1u)));
