@@ -1178,7 +1178,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
 // k_query tree waves: nodes per lane in flight on the wide row-shape levels and the leaf level
 // (1 = one AES chain per lane, the round-3 form; PIR_TREE_ILP at build time)
 #ifndef PIR_TREE_ILP
-#define PIR_TREE_ILP 1
+#define PIR_TREE_ILP 2
 #endif
 constexpr int kTreeIlp = PIR_TREE_ILP;
 constexpr int kQueryCwCap = 256;  // (levels x (p-1)) correction words staged in LDS
@@ -1275,6 +1275,8 @@ __global__ __launch_bounds__(NT) void k_query(
   }
   // atomic_red: the answers were zeroed by a memset the host enqueued before this launch (on
   // the same stream), so no workgroup waits on another's progress
+  const uint32_t tree_prio = (red_mode >> 8) & 3u;  // launch_query: $PIR_QUERY_TREE_PRIO
+  red_mode &= 0xffu;
   const bool atomic_red = out && red_mode == 2;
   const uint32_t red_groups = red_mode == 3 ? 8u : 1u;  // slab groups of the last-add reduce
   __syncthreads();
@@ -1290,6 +1292,10 @@ __global__ __launch_bounds__(NT) void k_query(
     fr_t += (size_t)b << (kQueryKin + ls);
   }
   const uint64_t region_rows = (uint64_t)TILE << lt;
+  // first row (in this engine's rows) of tile i of this workgroup
+  auto tile_row0 = [&](uint32_t i) __attribute__((always_inline)) -> uint64_t {
+    return (uint64_t)blockIdx.x * region_rows + (uint64_t)i * TILE;
+  };
   const size_t slab_words = (size_t)NQ * GW;
   const size_t slab_q_words = (size_t)gy * gridDim.x * slab_words;  // one query's slabs
 
@@ -1640,6 +1646,9 @@ __global__ __launch_bounds__(NT) void k_query(
   tree_tile(0, NT, NWV);  // every wave builds the first tile
   if (wave < (uint32_t)TW) {
     // ===================================== tree role ======================================
+    if (tree_prio == 3) __builtin_amdgcn_s_setprio(3);
+    else if (tree_prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (tree_prio == 1) __builtin_amdgcn_s_setprio(1);
     for (uint32_t g = 1; g < total; ++g) {
       // slot g % RING free: every scan wave has consumed tile g - RING (per-slot counts)
       if (g >= (uint32_t)RING) lds_wait_geq_idle(&sm.consumed[g % RING], (g / RING) * SW);
@@ -1690,7 +1699,7 @@ __global__ __launch_bounds__(NT) void k_query(
     constexpr bool kM4RExact = kM4R && SW == 8 && TILE == 1024 && 128 % U == 0;
     const bool scan = wi < nwg && !(trace && trace_flags_noscan);
     __builtin_amdgcn_s_setprio(PIR_SCAN_PRIO);
-    const uint8_t* rbase = shard + (b * region_rows) * pitch + (uint64_t)chunk * CH;
+    const uint8_t* rbase = shard + (uint64_t)chunk * CH;  // + tile_row0(i) rows
     // Rolling load pipeline: x[u] holds slot j0 + u; once it is folded, slot j0 + U + u is loaded
     // into it -- at the end of a tile, from the next tile (of this or the next query).  Shard rows
     // do not depend on the tree, so U rows per lane stay in flight across tiles and queries; only
@@ -1703,14 +1712,14 @@ __global__ __launch_bounds__(NT) void k_query(
     // 0 past the queue's last tile), the row's byte offset in soffset (wave-uniform), the lane's
     // chunk offset in voffset (lanes past the record read its first chunk) -- no per-lane 64-bit
     // address arithmetic, exec masking or branch per row.  TILE * pitch < 2^31 (make_query_plan).
-    const uint8_t* const rgn = shard + (b * region_rows) * pitch;
+
     const uint32_t lane_off = chunk < cpr ? chunk * CH : 0u;
     const uint32_t tile_bytes = (uint32_t)TILE * pitch;
     auto load_slot = [&](uint32_t g, uint32_t j, Chunk<VEC>& dst) __attribute__((always_inline)) {
       const uint32_t gi = wi + j * nwg;
       if constexpr (UNI) {
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(rgn + (uint64_t)(g & (ntiles - 1)) * tile_bytes), (short)0,
+            (void*)(shard + tile_row0(g & (ntiles - 1)) * pitch), (short)0,
             g < total ? (int)tile_bytes : 0, kBufRsrcWord3);
         // four-Russians scan waves at 8 per workgroup: nwg = 8 / gy divides 8, so with TILE =
         // 1024 rows and U | 128 every slot holds a row -- no guard, two SALU fewer per row
@@ -1718,7 +1727,7 @@ __global__ __launch_bounds__(NT) void k_query(
       } else {
         const uint32_t rl = gi * rpw + rec_off;
         const bool ok = g < total && active && gi < ngroups && rl < TILE;
-        dst = load_chunk<VEC>(ok ? rbase + ((uint64_t)(g & (ntiles - 1)) * TILE + rl) * pitch : shard);
+        dst = load_chunk<VEC>(ok ? rbase + (tile_row0(g & (ntiles - 1)) + rl) * pitch : shard);
       }
     };
     auto fold_row = [&](const Chunk<VEC>& xr, const uint4& c4) __attribute__((always_inline)) {
@@ -1760,7 +1769,7 @@ __global__ __launch_bounds__(NT) void k_query(
       const uint8_t* ring = sm.ring[g % RING];
       lds_wait_geq(&sm.ready, g + 1);
       if (!UNI && scan) {  // per-lane coefficients: batches of U rows of this tile
-        const uint8_t* base = rbase + ((uint64_t)i * TILE) * pitch;
+        const uint8_t* base = rbase + tile_row0(i) * pitch;
         for (uint32_t g0 = wi; g0 < ngroups; g0 += U * nwg) {
           Chunk<VEC> xb[U];
           uint4 cb[U];
@@ -2357,6 +2366,16 @@ hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_
   if (out && (red_mode < 1 || red_mode > 3 || (qp.lr < 3 && red_mode == 3))) return hipErrorInvalidValue;
   if (out && red_mode >= 2 && (efs % 4 != 0 || reinterpret_cast<uintptr_t>(out) % 4 != 0))
     return hipErrorInvalidValue;
+  // the tree waves' s_setprio after the first tile (0-3; the scan waves run at PIR_SCAN_PRIO),
+  // passed in red_mode's bits 8-9; $PIR_QUERY_TREE_PRIO (read per launch) overrides
+  // A lone query (nk == 1) is paced by its tree after the first tile, a queue by the scan:
+  // prio 3 for a lone query's tree waves, the default 0 in a queue (same box, configs[1] lone
+  // 0.2500 -> 0.2423 ms; a 2^24 x 1 KiB queue 2.55 -> 2.68 ms at prio 3:
+  // profiles/r04/bench_tree_prio.jsonl)
+  {
+    const char* tp = getenv("PIR_QUERY_TREE_PRIO");
+    red_mode |= ((tp ? (uint32_t)atoi(tp) : (nk == 1 ? 3u : 0u)) & 3u) << 8;
+  }
 #define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, scratch, s, trace, out, qcnt, efs, red_mode)
 #ifdef PIR_DEV_NQ  // development builds only (ISA / register checks): one round count
   return qp.shape.nq == PIR_DEV_NQ && qp.tile == 1024 ? PIR_Q(PIR_DEV_NQ, 1024) : hipErrorInvalidValue;

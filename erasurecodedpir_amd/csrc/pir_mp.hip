@@ -73,12 +73,19 @@ __device__ __forceinline__ uint4 load_cw(const uint8_t* key, uint64_t off, bool 
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// 1024-thread workgroups (16 waves per CU: the 64 KiB of tables allow one such workgroup per
+// CU, and R <= 4 counter blocks with NRP accumulators fit 128 VGPRs: R = 4 / 2 / 1 for
+// NRP = 1 / 2-4 / 8-16).  Round 4: at 256 threads, R = 4 and 180 VGPRs (NRP = 4) the LDS and
+// the registers held a CU to 8 waves, too few to hide the per-seed AES chains.
+constexpr int kMpThreads = 1024;
+
 template <int NRP, int R>
-__global__ __launch_bounds__(256) void k_mp_shares(const uint8_t* __restrict__ key, MpLayout L,
-                                                   uint64_t rec_lo, uint64_t rec_hi,
-                                                   uint8_t* __restrict__ d_c) {
+__global__ __launch_bounds__(kMpThreads) void k_mp_shares(const uint8_t* __restrict__ key,
+                                                          MpLayout L, uint64_t rec_lo,
+                                                          uint64_t rec_hi,
+                                                          uint8_t* __restrict__ d_c) {
   __shared__ uint32_t lds_tab[kTablesBytes / 4];
-  load_tables_n<256>(lds_tab);
+  load_tables_n<kMpThreads>(lds_tab);
   __syncthreads();
   const Tab T(lds_tab);
   const uint64_t W = L.mu < 16ull * R ? L.mu : 16ull * R;  // records per item
@@ -175,15 +182,18 @@ __global__ __launch_bounds__(256) void k_mp_shares(const uint8_t* __restrict__ k
 template <int NRP>
 hipError_t launch_nrp(const MpLayout& L, const uint8_t* d_key, uint64_t lo, uint64_t hi,
                       uint8_t* d_c, int num_cus, hipStream_t s) {
-  const bool r4 = L.mu >= 64;
-  const uint64_t W = r4 ? 64 : std::min<uint64_t>(L.mu, 16);
+  constexpr int RW = NRP <= 1 ? 4 : (NRP <= 4 ? 2 : 1);  // counter blocks per lane, wide rows
+  const bool wide = L.mu >= 16ull * RW;
+  const uint64_t W = wide ? 16ull * RW : std::min<uint64_t>(L.mu, 16);
   const uint64_t items = (hi + W - 1) / W - lo / W;
   const unsigned grid = (unsigned)std::max<uint64_t>(
-      1, std::min<uint64_t>((items + 255) / 256, (uint64_t)num_cus * 8));
-  if (r4)
-    hipLaunchKernelGGL((k_mp_shares<NRP, 4>), dim3(grid), dim3(256), 0, s, d_key, L, lo, hi, d_c);
+      1, std::min<uint64_t>((items + kMpThreads - 1) / kMpThreads, (uint64_t)num_cus * 2));
+  if (wide)
+    hipLaunchKernelGGL((k_mp_shares<NRP, RW>), dim3(grid), dim3(kMpThreads), 0, s, d_key, L, lo,
+                       hi, d_c);
   else
-    hipLaunchKernelGGL((k_mp_shares<NRP, 1>), dim3(grid), dim3(256), 0, s, d_key, L, lo, hi, d_c);
+    hipLaunchKernelGGL((k_mp_shares<NRP, 1>), dim3(grid), dim3(kMpThreads), 0, s, d_key, L, lo,
+                       hi, d_c);
   return hipGetLastError();
 }
 

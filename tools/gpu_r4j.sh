@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4, pass J: tree ILP A/B (k_query tree waves: 2 nodes per lane in flight on the wide
 # levels, PIR_TREE_ILP=2: libpir_engine_ilp2.so, against the one-chain default build), parity of
-# the ILP build (the gpu tests that pin k_query, run against it), and the region/tile read micro
+# the ILP build (the gpu tests that pin k_query, run against it)
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
@@ -14,4 +14,3 @@ for lib in ilp1 ilp2 ilp1 ilp2; do
   timeout -k 10 400 python -u bench.py --no-cpu >> gpurun_out/r4j_ab.jsonl 2>> gpurun_out/r4j_ab.err || exit $?
 done
 unset PIR_ENGINE_LIB
-timeout -k 10 300 tools/micro/read_regions > gpurun_out/r4j_read_regions.txt 2>&1
