@@ -241,7 +241,9 @@ int pir_comm_unique_id(uint8_t id[PIR_COMM_ID_BYTES]);
 int pir_comm_attach(pir_engine_t *e, const uint8_t id[PIR_COMM_ID_BYTES], int nranks, int rank);
 /* drop the communicator (aborted, never waited on) and answer this partition alone again; also
  * clears the refusal state after a failed exchange.  For callers that fall back to exchanging
- * partition answers themselves when a communicator could not be set up on every rank. */
+ * partition answers themselves when a communicator could not be set up on every rank.  Call it
+ * with no answer in flight: it waits for the engine's own stream only, and an exchange enqueued
+ * on a caller's stream would be cut off by the abort. */
 int pir_comm_detach(pir_engine_t *e);
 /* the combine step after the all-gather, on its own: d_gathered = nranks blocks of
  * bytes_per_rank (rank r's partial answers at r * bytes_per_rank: ncclAllGather's output
