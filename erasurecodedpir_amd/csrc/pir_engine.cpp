@@ -762,6 +762,25 @@ int answer_mp_locked(pir_engine* e, const pir::MpLayout& L, const uint8_t* d_key
   const size_t out_bytes = (size_t)c.num_rounds * c.record_bytes;
   uint8_t* out = e->comm ? e->d_part : d_result;
   e->ev = nullptr;
+  // the whole domain of a layout k_query tiles (the plan's tile divides mu; few seeds per row):
+  // ONE launch, its tree waves building each tile's shares from the key while the scan waves
+  // stream the shard ($PIR_MP_FUSED=1, under test; else k_mp_shares, then the scan)
+  if (thread_num == 0 && num_threads == 1 && L.nu && L.p2 <= 64 && e->allow_query) {
+    const char* fv = getenv("PIR_MP_FUSED");
+    const pir::QueryPlan qp = pir::make_query_plan(c.log_num_records, c.log_num_partitions, 2,
+                                                   c.num_rounds, e->pitch, e->num_cus);
+    if (fv && atoi(fv) == 1 && qp.tile && qp.shape.uniform && L.mu % (uint64_t)qp.tile == 0) {
+      if (int rc = ensure_slabs(e, pir::query_slab_bytes(qp))) return rc;
+      HIP_TRY(pir::launch_query_mp(qp, d_key, 0, 1, L, c.log_num_records, c.log_num_partitions,
+                                   (uint64_t)c.partition_index, e->d_shard, e->d_slabs, s));
+      HIP_TRY(pir::launch_reduce(qp.shape, e->d_slabs, c.record_bytes, out, s));
+      e->last_fused = 3;
+      if (e->comm) {
+        if (int rc = exchange(e, e->d_part, out_bytes, e->d_gather, d_result, s)) return rc;
+      }
+      return PIR_OK;
+    }
+  }
   const uint64_t slice = L.nu / (uint64_t)num_threads;
   const uint64_t p0 = (uint64_t)c.partition_index * e->rows;
   const uint64_t lo = std::max<uint64_t>((uint64_t)thread_num * slice * L.mu, p0);

@@ -166,7 +166,7 @@ struct QueryPlan {
   int tile, lr, lt;
   int ls;           // 2^ls tiles per super-tile (their narrow top levels expanded once)
   int tw;           // tree waves per workgroup (the rest scan)
-  int m4r;          // 4-5 rounds: the 768-thread four-Russians k_query (1: kM4rTW tree waves, 2: two)
+  int m4r;          // 3-5 rounds: the 768-thread four-Russians k_query (1: kM4rTW tree waves, 2: two)
   ScanShape shape;  // grid.x = 2^lr workgroups (slabs), grid.y = column groups
 };
 QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, int num_cus,
@@ -187,6 +187,14 @@ hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_
                         const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
                         uint64_t* trace = nullptr, uint8_t* out = nullptr,
                         uint32_t* qcnt = nullptr, uint32_t efs = 0, uint32_t red_mode = 0);
+// k_query for a sqrt(N) DPF key (multiparty / covering design, pir_mp.h's MpLayout): the tree
+// waves build each tile's shares from the key's seeds, toggles and correction words (mp_tile)
+// while the scan waves stream the shard; then launch_reduce as for launch_query.  nk keys
+// key_stride bytes apart (16-aligned), L.nrk == the plan's rounds, the plan's tile divides L.mu.
+struct MpLayout;
+hipError_t launch_query_mp(const QueryPlan& qp, const uint8_t* d_key, uint32_t key_stride,
+                           int nk, const MpLayout& L, int n, int log_parts, uint64_t prefix,
+                           const uint8_t* shard, uint8_t* slabs, hipStream_t s);
 // XOR the slabs, compact pitch -> record_bytes: d_out[a*efs + b]; nk queries (slabs of query k
 // grid.x*grid.y*slab_bytes apart, answers nq*efs bytes apart).  nslices > 1 (dividing grid.x):
 // per query, nslices answers over consecutive equal runs of the grid.x slabs, i.e. over equal

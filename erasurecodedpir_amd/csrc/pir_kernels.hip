@@ -18,6 +18,7 @@
 #include "pir_aes.h"
 #include "pir_tree.h"
 #include "pir_m4r.h"
+#include "pir_mp.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -1232,15 +1233,90 @@ __device__ __forceinline__ void stage_key(const uint8_t* __restrict__ raw, int p
   }
 }
 
+// The shares of records [rec0, rec0 + TILE) of a sqrt(N) DPF key (multiparty or covering
+// design, the layout of pir_mp.h: share a of record i*mu + x = XOR over the row's seeds j with
+// toggle (a, i, j) set of G(s[i][j], mu)[x] ^ cw[j][x]; multiparty_dpf.cpp:590-601, :665-675)
+// into a k_query ring slot ([record][NRP] bytes), by the first nt threads: lpi lanes per CTR
+// block of the tile (16 records) split the row's seeds, then XOR their partials.  TILE | mu.
+template <int TILE, int NRP>
+__device__ __forceinline__ void mp_tile(const Tab& T, const uint8_t* __restrict__ key,
+                                        const MpLayout& L, uint64_t rec0, uint8_t* ring, int tt,
+                                        int nt) {
+  constexpr int NB = TILE / 16;
+  int lpi = 1;
+  while (lpi * 2 * NB <= nt) lpi *= 2;
+  const int blk = tt / lpi, sub = tt & (lpi - 1);
+  const bool act = blk < NB;
+  const uint64_t ri = rec0 / L.mu;
+  const uint32_t bc = (uint32_t)((rec0 - ri * L.mu) >> 4) + (uint32_t)(act ? blk : 0);
+  const uint64_t row_tog = L.nu * L.p2;
+  const bool cw_al = (L.cw_off & 15) == 0;
+  uint4 acc[NRP];
+#pragma unroll
+  for (int a = 0; a < NRP; ++a) acc[a] = make_uint4(0, 0, 0, 0);
+  if (act) {
+    for (uint32_t j = (uint32_t)sub; j < L.p2; j += (uint32_t)lpi) {
+      uint32_t m[NRP];
+      uint32_t any = 0;
+#pragma unroll
+      for (int a = 0; a < NRP; ++a) {
+        m[a] = (a < L.nrk && key[L.tog_off + a * row_tog + ri * L.p2 + j]) ? ~0u : 0u;
+        any |= m[a];
+      }
+      if (!any) continue;
+      const uint4 seed = *reinterpret_cast<const uint4*>(key + ri * 16ull * L.p2 + 16ull * j);
+      uint4 o[1];
+      aes_ctr_row<1, 4>(T, seed, o, __builtin_bswap32(bc));
+      const uint8_t* cwp = key + L.cw_off + (uint64_t)j * L.mu + 16ull * bc;
+      uint4 cw;
+      if (cw_al) {
+        cw = *reinterpret_cast<const uint4*>(cwp);
+      } else {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 16; ++k) w[k >> 2] |= (uint32_t)cwp[k] << (8 * (k & 3));
+        cw = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      const uint4 v = xor4(o[0], cw);
+#pragma unroll
+      for (int a = 0; a < NRP; ++a) acc[a] = xor4(acc[a], and4(v, m[a]));
+    }
+  }
+  for (int off = 1; off < lpi; off <<= 1) {  // the lpi lanes of a block are adjacent
+#pragma unroll
+    for (int a = 0; a < NRP; ++a) {
+      acc[a].x ^= (uint32_t)__shfl_xor((int)acc[a].x, off, 64);
+      acc[a].y ^= (uint32_t)__shfl_xor((int)acc[a].y, off, 64);
+      acc[a].z ^= (uint32_t)__shfl_xor((int)acc[a].z, off, 64);
+      acc[a].w ^= (uint32_t)__shfl_xor((int)acc[a].w, off, 64);
+    }
+  }
+  if (act && sub == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int a = 0; a < NRP; ++a) {
+        const uint32_t wd = (k >> 2) == 0 ? acc[a].x : (k >> 2) == 1 ? acc[a].y
+                          : (k >> 2) == 2 ? acc[a].z : acc[a].w;
+        w[a >> 2] |= ((wd >> (8 * (k & 3))) & 0xffu) << (8 * (a & 3));
+      }
+      store_leaf<NRP>(ring, (uint64_t)(16 * blk + k), make_uint4(w[0], w[1], w[2], w[3]));
+    }
+  }
+}
+
 template <int NQ, int NRP, int VEC, bool UNI, int TW, int TILE, int GYMAX, int RING,
-          int NT = kFusedThreads>
+          int NT = kFusedThreads, bool MPK = false>
 __global__ __launch_bounds__(NT) void k_query(
     const uint8_t* __restrict__ raw0, uint32_t key_stride, int nk, int p, int n, int nq,
     int party0, int log_parts, uint64_t prefix, int lr, int lt, int ls,
     uint4* __restrict__ fr_s, uint32_t* __restrict__ fr_t, const uint8_t* __restrict__ shard,
     uint32_t pitch, uint32_t cpr, uint32_t gy, uint8_t* __restrict__ slabs,
     uint64_t* __restrict__ trace, uint8_t* __restrict__ out, uint32_t* __restrict__ qcnt,
-    uint32_t efs, uint32_t red_mode) {
+    uint32_t efs, uint32_t red_mode, MpLayout mpl) {
+  // MPK: the queue's keys are sqrt(N) DPF keys of layout mpl (key_stride bytes apart; multiparty
+  // or covering design), and the tree waves build each tile's shares with mp_tile instead of a
+  // DPF tree; the scan waves, slabs and reduce are the same
   // out != nullptr: the slabs of each query are reduced in-kernel into out (query k at
   // out + k * nq * efs); else the host launches k_reduce.  red_mode 1: the last workgroup to
   // add to qcnt[k] (zero on entry, left zero) XORs every slab.  Modes 2 and 3 (efs % 4 == 0,
@@ -1268,7 +1344,7 @@ __global__ __launch_bounds__(NT) void k_query(
   const uint32_t pm1 = (uint32_t)p - 1;
   load_tables_n<NT>(sm.tab);
   for (int i = threadIdx.x; i < GYMAX * NQ * GW; i += blockDim.x) (&sm.red[0][0])[i] = 0;
-  stage_key(raw0, p, n, nq, threadIdx.x, NT, sm.scw, sm.tcw, sm.lastcw);
+  if constexpr (!MPK) stage_key(raw0, p, n, nq, threadIdx.x, NT, sm.scw, sm.tcw, sm.lastcw);
   if (threadIdx.x == 0) {
     sm.bar = 0; sm.sbar = 0; sm.ready = 0;
     for (int r = 0; r < RING; ++r) sm.consumed[r] = 0;
@@ -1334,6 +1410,13 @@ __global__ __launch_bounds__(NT) void k_query(
       if (team == (uint32_t)NWV) __syncthreads();
       else group_barrier(&sm.bar, gen, team);
     };
+    if constexpr (MPK) {  // a sqrt(N) DPF key's shares instead of a DPF tree
+      mp_tile<TILE, NRP>(T, raw, mpl, ((uint64_t)prefix << (n - log_parts)) + tile_row0(i), ring,
+                         tt, nt);
+      sync();  // every share of tile g is in the ring
+      if (wave == 0) lds_signal(&sm.ready);
+      return;
+    }
     if (i == 0 && g > 0) {  // next query: its key replaces the previous one's (all tree waves
       stage_key(raw, p, n, nq, tt, nt, sm.scw, sm.tcw, sm.lastcw);  // are past its last use)
       sync();
@@ -1687,7 +1770,7 @@ __global__ __launch_bounds__(NT) void k_query(
     // rounds, else masks from the plane table (8 v_bitop3 with an SGPR mask, 2/3 the issue rate)
     // 768-thread workgroups (4 to 5 rounds): four Russians over groups of 4 rows (pir_m4r.h:
     // 2.5x fewer VALU ops than the masks, 32 more VGPRs -- which 16 waves per CU do not have)
-    constexpr bool kM4R = UNI && VEC == 2 && NQ >= 4 && NQ <= 5 && NT == kM4rThreads;
+    constexpr bool kM4R = UNI && VEC == 2 && NQ >= 3 && NQ <= 5 && NT == kM4rThreads;
     constexpr bool kPlaneAsm = !kM4R && UNI && VEC == 2 && NQ >= 3 && NQ > PIR_QUERY_BRANCH_MAXNQ;
     // rows in flight per lane (one record per wave row: a rolling pipeline whose x[] stays live
     // across tiles; several records per row: U rows loaded, then folded, per batch)
@@ -2280,10 +2363,12 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
     const int v = atoi(tw);
     if (v == kFusedTW || (v == kQueryTreeHeavyTW && nq <= 2)) qp.tw = v;
   }
-  // 4-5 rounds at VEC 2 with one record per wave row: the four-Russians k_query (768 threads:
-  // 4 tree + 8 scan waves) unless $PIR_QUERY_M4R=0
+  // 3-5 rounds at VEC 2 with one record per wave row: the four-Russians k_query (768 threads:
+  // 4 tree + 8 scan waves) unless $PIR_QUERY_M4R=0.  Round 4 added 3 rounds: the plane-mask
+  // k_query ran a 2^24 x 1 KiB query at 4.40 ms (3.9 TB/s) against 3.44 at 4 rounds with the
+  // fold (profiles/r04/probe_rounds*.txt)
   if ((uint64_t)tile * pitch >= (1ull << 31)) return qp;  // a tile's rows: one buffer resource
-  qp.m4r = nq >= 4 && nq <= 5 && nq > PIR_QUERY_BRANCH_MAXNQ && tile == 1024 &&
+  qp.m4r = nq >= 3 && nq <= 5 && nq > PIR_QUERY_BRANCH_MAXNQ && tile == 1024 &&
            pitch / 8 >= (uint32_t)kColGroupLanes;
   if (const char* mv = getenv("PIR_QUERY_M4R")) qp.m4r = qp.m4r && atoi(mv) != 0;
   // diagnostics: $PIR_QUERY_M4R_TW=2 -> 2 tree + 10 scan waves (default 4 + 8)
@@ -2330,9 +2415,9 @@ static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t k
   hipLaunchKernelGGL((k_query<NQ, NRP, VEC, UNI, TW, TILE, GY, RING, NTH>), dim3(sh.grid.x),     \
                      dim3(NTH), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,                    \
                      log_parts, prefix, qp.lr, qp.lt, qp.ls, fr_s, fr_t, shard, sh.pitch, sh.cpr,  \
-                     gy, slabs, trace, out, qcnt, efs, red_mode)
+                     gy, slabs, trace, out, qcnt, efs, red_mode, MpLayout{})
 #define PIR_QL(UNI, TW, GY, gy) PIR_QLN(UNI, TW, GY, gy, kFusedThreads)
-  if constexpr (VEC == 2 && NQ >= 4 && NQ <= 5 && NQ > PIR_QUERY_BRANCH_MAXNQ && TILE == 1024) {
+  if constexpr (VEC == 2 && NQ >= 3 && NQ <= 5 && NQ > PIR_QUERY_BRANCH_MAXNQ && TILE == 1024) {
     if (sh.uniform && qp.m4r) {  // four-Russians scan waves (k_query's kM4R)
       if (qp.m4r == 2) PIR_QLN(true, 2, 4, sh.grid.y, kM4rThreads);  // diagnostics: 2 tree waves
       else PIR_QLN(true, kM4rTW, 4, sh.grid.y, kM4rThreads);
@@ -2351,6 +2436,59 @@ static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t k
 #undef PIR_QL
 #undef PIR_QLN
   return hipGetLastError();
+}
+
+// k_query in its sqrt(N) DPF mode (MPK): mp_tile builds each tile's shares from the key
+template <int NQ, int TILE>
+static hipError_t query_nq_mp(const QueryPlan& qp, const uint8_t* d_key, uint32_t key_stride,
+                              int nk, const MpLayout& L, int n, int log_parts, uint64_t prefix,
+                              const uint8_t* shard, uint8_t* slabs, hipStream_t s) {
+  constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : 8));
+  constexpr int VEC = NQ <= 2 ? 4 : 2;
+  constexpr int RING = TILE == 4096 ? 2 : 4;
+  const ScanShape& sh = qp.shape;
+  if (!sh.uniform) return hipErrorInvalidValue;
+  // tree-wave priority as launch_query (a lone query's share waves at 3)
+  const char* tp = getenv("PIR_QUERY_TREE_PRIO");
+  const uint32_t rm = ((tp ? (uint32_t)atoi(tp) : (nk == 1 ? 3u : 0u)) & 3u) << 8;
+#define PIR_QMP(TW, NTH)                                                                         \
+  hipLaunchKernelGGL((k_query<NQ, NRP, VEC, true, TW, TILE, 4, RING, NTH, true>),               \
+                     dim3(sh.grid.x), dim3(NTH), 0, s, d_key, key_stride, nk, 2, n, NQ, 0,       \
+                     log_parts, prefix, qp.lr, qp.lt, 0, nullptr, nullptr, shard, sh.pitch,      \
+                     sh.cpr, sh.grid.y, slabs, nullptr, nullptr, nullptr, 0u, rm, L)
+  if constexpr (VEC == 2 && NQ >= 3 && NQ <= 5 && NQ > PIR_QUERY_BRANCH_MAXNQ && TILE == 1024) {
+    if (qp.m4r) {
+      PIR_QMP(kM4rTW, kM4rThreads);
+      return hipGetLastError();
+    }
+  }
+  PIR_QMP(kFusedTW, kFusedThreads);
+#undef PIR_QMP
+  return hipGetLastError();
+}
+
+hipError_t launch_query_mp(const QueryPlan& qp, const uint8_t* d_key, uint32_t key_stride,
+                           int nk, const MpLayout& L, int n, int log_parts, uint64_t prefix,
+                           const uint8_t* shard, uint8_t* slabs, hipStream_t s) {
+  if (nk < 1 || !qp.tile || !L.nu || L.mu % (uint64_t)qp.tile != 0 || L.nrk != qp.shape.nq)
+    return hipErrorInvalidValue;
+#define PIR_QM(NQ, TL) query_nq_mp<NQ, TL>(qp, d_key, key_stride, nk, L, n, log_parts, prefix, shard, slabs, s)
+  const int nq = qp.shape.nq;
+  if (qp.tile == 4096) {
+    if (nq == 1) return PIR_QM(1, 4096);
+    if (nq == 2) return PIR_QM(2, 4096);
+    return hipErrorInvalidValue;
+  }
+  if (qp.tile != 1024) return hipErrorInvalidValue;
+  switch (nq) {
+    case 1: return PIR_QM(1, 1024);
+    case 2: return PIR_QM(2, 1024);
+    case 3: return PIR_QM(3, 1024);
+    case 4: return PIR_QM(4, 1024);
+    case 5: return PIR_QM(5, 1024);
+    default: return hipErrorInvalidValue;
+  }
+#undef PIR_QM
 }
 
 size_t query_scratch_bytes(const QueryPlan& qp) {
