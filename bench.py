@@ -967,6 +967,9 @@ def run_mp(args, ctx, config):
     else:
         ans_dev = lambda dk, dr: eng.answer_mp_dev(dk, p, t, dr)  # noqa: E731
         ans = lambda k: eng.answer_mp(k, p, t)  # noqa: E731
+    # the engine's default (answer_mp_locked): k_query's sqrt(N) mode for >= 3 shares
+    fv = os.environ.get("PIR_MP_FUSED", "1")
+    fused = fv == "2" or (fv != "0" and nrk >= 3)
     eng = pir.Engine(2, 1, n, efs, nrk, device=ctx.local)
     eng.fill_shard_random(SHARD_SEED)
     d_k = eng.alloc_dev(nkeys * eb)
@@ -1005,9 +1008,13 @@ def run_mp(args, ctx, config):
                       **({"num_cd_keys_needed": qn} if cd else {"parties": p, "threshold": t}),
                       "shares": nrk, "seeds_per_row": p2, "row_records": mu,
                       "rows": nu, "key_bytes_read": eb,
-                      "step": "one query: k_mp_shares (AES-CTR per seed, toggled into the shares) "
-                              "+ k_scan + k_reduce"},
-           "roofline": {"bound": "hbm", "kernel": "k_mp_shares + k_scan + k_reduce",
+                      "step": "one query: >= 3 shares: k_query in its sqrt(N) mode (the tree "
+                              "waves build each tile's shares -- AES-CTR per seed, toggled into "
+                              "the shares -- while the scan waves stream the shard) + k_reduce; "
+                              "2 shares or PIR_MP_FUSED=0: k_mp_shares + k_scan_uni + k_reduce",
+                      "mp_fused": fused},
+           "roofline": {"bound": "hbm", "kernel": "k_query (sqrt(N) mode) + k_reduce" if fused
+                        else "k_mp_shares + k_scan_uni + k_reduce",
                         "achieved": round(algo / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                         "traffic": None, "algorithmic_bytes_per_query": int(algo),

@@ -764,12 +764,22 @@ int answer_mp_locked(pir_engine* e, const pir::MpLayout& L, const uint8_t* d_key
   e->ev = nullptr;
   // the whole domain of a layout k_query tiles (the plan's tile divides mu; few seeds per row):
   // ONE launch, its tree waves building each tile's shares from the key while the scan waves
-  // stream the shard ($PIR_MP_FUSED=1, under test; else k_mp_shares, then the scan)
-  if (thread_num == 0 && num_threads == 1 && L.nu && L.p2 <= 64 && e->allow_query) {
-    const char* fv = getenv("PIR_MP_FUSED");
+  // stream the shard.  $PIR_MP_FUSED: 0 = never (k_mp_shares, then the scan), 2 = always (an
+  // answer k_query cannot take fails: tests), default: where it applies and has >= 3 shares.
+  // Measured on 2^24 x 1 KiB (profiles/r04/r4o_ab.jsonl, r4p_ab.jsonl): CD842 (3 shares)
+  // 3.19 -> 2.87 ms, CD732 (4) 4.19 -> 3.78 ms; multiparty p = 3 (2 shares) 2.70 -> 2.77 ms, so
+  // 2 shares keep the two-kernel path (its scan alone runs at 0.80 of HBM peak)
+  const char* fv = getenv("PIR_MP_FUSED");
+  const int fmode = fv ? atoi(fv) : 1;
+  if (fmode != 0) {
     const pir::QueryPlan qp = pir::make_query_plan(c.log_num_records, c.log_num_partitions, 2,
                                                    c.num_rounds, e->pitch, e->num_cus);
-    if (fv && atoi(fv) == 1 && qp.tile && qp.shape.uniform && L.mu % (uint64_t)qp.tile == 0) {
+    const bool takes = thread_num == 0 && num_threads == 1 && L.nu && L.p2 <= 64 &&
+                       e->allow_query && qp.tile && qp.shape.uniform &&
+                       L.mu % (uint64_t)qp.tile == 0 && (fmode == 2 || L.nrk >= 3);
+    if (!takes && fmode == 2)
+      return fail(PIR_EINVAL, "k_query's sqrt(N) mode does not take this answer ($PIR_MP_FUSED=2)");
+    if (takes) {
       if (int rc = ensure_slabs(e, pir::query_slab_bytes(qp))) return rc;
       HIP_TRY(pir::launch_query_mp(qp, d_key, 0, 1, L, c.log_num_records, c.log_num_partitions,
                                    (uint64_t)c.partition_index, e->d_shard, e->d_slabs, s));

@@ -179,3 +179,36 @@ def test_gpu_cd_rejects_bad_arguments():
             e.answer_cd(key, 6, 3, 4, 4)  # thread 4 of 4
         with pytest.raises(pir.PirError):
             e.answer_cd(key, 0, 3)  # no layout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,a,b,nrk,n,efs", [
+    # n >= 19: k_query takes a domain of >= 2 tiles of 1024 leaves per CU (fused_tile)
+    ("cd", 6, 3, 3, 19, 1024),    # CD842 counts: 32 seeds a row of 4096 records, 3 shares
+    ("cd", 7, 4, 4, 20, 512),     # CD732 counts: 64 seeds, 4 shares (the four-Russians k_query)
+    ("mp", 3, 1, 2, 19, 1024),    # multiparty p = 3, t = 1: 4 seeds a row of 2048 records
+    ("mp", 4, 1, 3, 19, 1040),    # p = 4: 8 seeds, 3 shares, ragged records
+])
+def test_gpu_sqrtn_in_k_query(kind, a, b, nrk, n, efs, monkeypatch):
+    """Whole-domain multiparty / covering-design answers through k_query's sqrt(N) mode
+    ($PIR_MP_FUSED=2: forced, an answer it cannot take fails; the tree waves build each tile's
+    shares from the key, mp_tile) == the two-kernel path ($PIR_MP_FUSED=0: k_mp_shares + the
+    scan) == the oracle, twice on one engine."""
+    import erasurecodedpir_amd as pir
+    if kind == "cd":
+        key = O.cd_key(n, a, b, 77 * n + a)
+        want = lambda k, sh: O.cd_answer(n, a, b, efs, k, sh)  # noqa: E731
+    else:
+        key = O.mp_key(a, n, b, 55 * n + a)
+        want = lambda k, sh: O.mp_answer(a, b, n, efs, k, sh)  # noqa: E731
+    shard = O.xorshift(3 * n + nrk, (1 << n) * efs)
+    got = {}
+    for mode in ("2", "0"):
+        monkeypatch.setenv("PIR_MP_FUSED", mode)
+        with pir.Engine(2, 1, n, efs, nrk) as e:
+            e.set_shard(shard)
+            ans = (lambda k: e.answer_cd(k, a, b)) if kind == "cd" else (lambda k: e.answer_mp(k, a, b))
+            got[mode] = [ans(key), ans(key)]
+    assert np.array_equal(got["2"][0], got["2"][1])
+    assert np.array_equal(got["2"][0], got["0"][0])
+    assert np.array_equal(got["2"][0], want(key, shard))
