@@ -691,12 +691,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras:
         out["configs1_c2"] = extra_leg(ctx, pir, "c2", W, K, rng)
         if config != "c4":
-            out["c4_single_engine"] = extra_leg(ctx, pir, "c4", min(W, 2), min(K, 8), rng,
+            out["c4_single_engine"] = extra_leg(ctx, pir, "c4", min(W, 2), min(K, 16), rng,
                                                 single=False)
         if config != "c5":
-            out["configs4_c5"] = extra_leg(ctx, pir, "c5", min(W, 2), min(K, 10), rng,
+            out["configs4_c5"] = extra_leg(ctx, pir, "c5", min(W, 3), min(K, 20), rng,
                                            single=False)
-        b = measure_batch(min(K, 3), min(W, 1), ctx, "c3b")
+        b = measure_batch(min(K, 8), min(W, 2), ctx, "c3b")
         out["configs2_c3b"] = {k: b[k] for k in ("value", "unit", "value_kind", "steps", "warmup",
                                                  "ms_per_step", "ms_per_key", "keys_per_s",
                                                  "shard_passes_per_step", "parity")}
