@@ -212,3 +212,36 @@ def test_gpu_sqrtn_in_k_query(kind, a, b, nrk, n, efs, monkeypatch):
     assert np.array_equal(got["2"][0], got["2"][1])
     assert np.array_equal(got["2"][0], got["0"][0])
     assert np.array_equal(got["2"][0], want(key, shard))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,a,b,nrk", [
+    ("cd", 6, 3, 3),   # the bench's ccd: CD842 counts, four-Russians k_query at 3 shares
+    ("cd", 7, 4, 4),   # ccd7: CD732 counts
+    ("mp", 4, 1, 3),   # cm4: multiparty p = 4, t = 1
+])
+def test_gpu_sqrtn_fullsize(kind, a, b, nrk, monkeypatch):
+    """At the bench shape (2^24 x 1 KiB, device-generated shard): k_query's sqrt(N) mode (the
+    default for >= 3 shares) == the two-kernel path == the XOR of 4 thread slices (which always
+    take the two-kernel path) -- the same answer by three routes; the oracle pins both paths at
+    2^19-2^20 (test_gpu_sqrtn_in_k_query)."""
+    import erasurecodedpir_amd as pir
+    n, efs = 24, 1024
+    key = O.cd_key(n, a, b, 5 + a) if kind == "cd" else O.mp_key(a, n, b, 9 + a)
+    with pir.Engine(2, 1, n, efs, nrk) as e:
+        e.fill_shard_random(11)
+        ans = (lambda *s: e.answer_cd(key, a, b, *s)) if kind == "cd" else (lambda *s: e.answer_mp(key, a, b, *s))
+        monkeypatch.setenv("PIR_MP_FUSED", "2")
+        fused = ans()
+        monkeypatch.setenv("PIR_MP_FUSED", "0")
+        two = ans()
+        monkeypatch.delenv("PIR_MP_FUSED")
+        dflt = ans()
+        sl = [ans(t, 4) for t in range(4)]
+    acc = np.zeros_like(two)
+    for s in sl:
+        acc ^= s
+    assert fused.any()
+    assert np.array_equal(fused, two)
+    assert np.array_equal(dflt, fused)
+    assert np.array_equal(acc, two)
