@@ -46,6 +46,16 @@ def main():
         raw = tr * 100.0  # back to ticks for the clock columns
         ghz = (raw[:, 57] - raw[:, 56]) / ((tr[:, 2] - tr[:, 0]) * 1e3)
         print(f"  shader clock start->first root: med {np.median(ghz):.3f} GHz (min {ghz.min():.3f} max {ghz.max():.3f})")
+        # workgroup b runs on XCD b % 8 under round-robin dispatch: per-XCD medians of the late
+        # phases and of the clock, and the spread of the end stamp within each XCD
+        names = list(e.TRACE_PHASES)
+        il, ie = names.index("last_tile_ready"), names.index("end")
+        xcd = np.arange(tr.shape[0]) % 8
+        for x in range(8):
+            m = xcd == x
+            print(f"  xcd {x}: last_tile_ready med {np.median(tr[m, il]):8.1f}  end med {np.median(tr[m, ie]):8.1f}"
+                  f" (min {tr[m, ie].min():8.1f} max {tr[m, ie].max():8.1f})  clock med {np.median(ghz[m]):.3f} GHz")
+        print(f"  corr(end, clock) over workgroups: {np.corrcoef(tr[:, ie], ghz)[0, 1]:+.2f}")
         if a.queue > 1:
             rd = [med[64 + g] for g in range(32) if tr[:, 64 + g].all()]
             cs = [med[96 + g] for g in range(32) if tr[:, 96 + g].all()]
