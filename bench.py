@@ -1001,6 +1001,9 @@ def run_mp(args, ctx, config):
     eng.close()
     gib = float(N) * efs / GIB
     algo = float(N) * efs + eb  # shard + the key
+    # HBM bytes of the sqrt(N) k_query from its committed counters (profiles/pmc_<config>.json,
+    # one query per launch; the shares never leave the CU), stamped with the library sha
+    traffic, tsrc = _pmc_traffic(config, ctx.world, 1) if fused else (None, None)
     out = {"metric": METRIC, "value": round(gib / (ms / 1e3), 3), "unit": "GiB/s", "n_gpus": 1,
            "steps": K, "warmup": W, "ms_per_step": r5(ms), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
@@ -1017,8 +1020,9 @@ def run_mp(args, ctx, config):
                         else "k_mp_shares + k_scan_uni + k_reduce",
                         "achieved": round(algo / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                        "traffic": None, "algorithmic_bytes_per_query": int(algo),
-                        "note": "wall time per query over the device work of all three launches"},
+                        "traffic": traffic, "traffic_source": tsrc,
+                        "algorithmic_bytes_per_query": int(algo),
+                        "note": "wall time per query over the device work of the launches"},
            "parity": {"correction_word_linearity": ok, "device_equals_host_api": ok_dev}}
     if ctx.rank == 0:
         print(json.dumps(out), flush=True)
