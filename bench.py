@@ -967,9 +967,10 @@ def run_mp(args, ctx, config):
     else:
         ans_dev = lambda dk, dr: eng.answer_mp_dev(dk, p, t, dr)  # noqa: E731
         ans = lambda k: eng.answer_mp(k, p, t)  # noqa: E731
-    # the engine's default (answer_mp_locked): k_query's sqrt(N) mode for >= 3 shares
+    # the engine's default (answer_mp_locked): k_query's sqrt(N) mode for >= 3 shares or <= 8
+    # seeds a row
     fv = os.environ.get("PIR_MP_FUSED", "1")
-    fused = fv == "2" or (fv != "0" and nrk >= 3)
+    fused = fv == "2" or (fv != "0" and (nrk >= 3 or p2 <= 8))
     eng = pir.Engine(2, 1, n, efs, nrk, device=ctx.local)
     eng.fill_shard_random(SHARD_SEED)
     d_k = eng.alloc_dev(nkeys * eb)
@@ -1011,10 +1012,11 @@ def run_mp(args, ctx, config):
                       **({"num_cd_keys_needed": qn} if cd else {"parties": p, "threshold": t}),
                       "shares": nrk, "seeds_per_row": p2, "row_records": mu,
                       "rows": nu, "key_bytes_read": eb,
-                      "step": "one query: >= 3 shares: k_query in its sqrt(N) mode (the tree "
-                              "waves build each tile's shares -- AES-CTR per seed, toggled into "
-                              "the shares -- while the scan waves stream the shard) + k_reduce; "
-                              "2 shares or PIR_MP_FUSED=0: k_mp_shares + k_scan_uni + k_reduce",
+                      "step": "one query: >= 3 shares or <= 8 seeds a row: k_query in its "
+                              "sqrt(N) mode (share waves build each tile's shares -- AES-CTR per "
+                              "seed, toggled into the shares -- while the scan waves stream the "
+                              "shard) + k_reduce; else or PIR_MP_FUSED=0: k_mp_shares + "
+                              "k_scan_uni + k_reduce",
                       "mp_fused": fused},
            "roofline": {"bound": "hbm", "kernel": "k_query (sqrt(N) mode) + k_reduce" if fused
                         else "k_mp_shares + k_scan_uni + k_reduce",

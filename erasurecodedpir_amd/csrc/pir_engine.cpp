@@ -765,10 +765,11 @@ int answer_mp_locked(pir_engine* e, const pir::MpLayout& L, const uint8_t* d_key
   // the whole domain of a layout k_query tiles (the plan's tile divides mu; few seeds per row):
   // ONE launch, its tree waves building each tile's shares from the key while the scan waves
   // stream the shard.  $PIR_MP_FUSED: 0 = never (k_mp_shares, then the scan), 2 = always (an
-  // answer k_query cannot take fails: tests), default: where it applies and has >= 3 shares.
-  // Measured on 2^24 x 1 KiB (profiles/r04/r4o_ab.jsonl, r4p_ab.jsonl): CD842 (3 shares)
-  // 3.19 -> 2.87 ms, CD732 (4) 4.19 -> 3.78 ms; multiparty p = 3 (2 shares) 2.70 -> 2.77 ms, so
-  // 2 shares keep the two-kernel path (its scan alone runs at 0.80 of HBM peak)
+  // answer k_query cannot take fails: tests), default: where it applies with >= 3 shares, or
+  // with 1-2 shares and <= 8 seeds a row (4 share waves + 12 scan waves, query_nq_mp).
+  // Measured on 2^24 x 1 KiB (profiles/r04/r4o_ab.jsonl, r4q_ab.jsonl, r4ae_ab.jsonl): CD842 (3
+  // shares) 3.19 -> 2.79 ms, CD732 (4) 4.19 -> 3.67 ms, multiparty p = 3 (2 shares, 4 seeds)
+  // 2.70 -> 2.52 ms (with 8 share waves it was 2.77: r4p_ab.jsonl)
   const char* fv = getenv("PIR_MP_FUSED");
   const int fmode = fv ? atoi(fv) : 1;
   if (fmode != 0) {
@@ -776,7 +777,8 @@ int answer_mp_locked(pir_engine* e, const pir::MpLayout& L, const uint8_t* d_key
                                                    c.num_rounds, e->pitch, e->num_cus);
     const bool takes = thread_num == 0 && num_threads == 1 && L.nu && L.p2 <= 64 &&
                        e->allow_query && qp.tile && qp.shape.uniform &&
-                       L.mu % (uint64_t)qp.tile == 0 && (fmode == 2 || L.nrk >= 3);
+                       L.mu % (uint64_t)qp.tile == 0 &&
+                       (fmode == 2 || L.nrk >= 3 || L.p2 <= 8);
     if (!takes && fmode == 2)
       return fail(PIR_EINVAL, "k_query's sqrt(N) mode does not take this answer ($PIR_MP_FUSED=2)");
     if (takes) {

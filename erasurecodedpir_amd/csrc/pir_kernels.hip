@@ -2462,6 +2462,15 @@ static hipError_t query_nq_mp(const QueryPlan& qp, const uint8_t* d_key, uint32_
       return hipGetLastError();
     }
   }
+  // 1-2 shares: few seeds per row (p2 <= 8) build a tile's shares in a fraction of the scan's
+  // time, so 4 share waves + 12 scan waves ($PIR_MP_TW=8: the tree DPF's 8 + 8)
+  if constexpr (NQ <= 2) {
+    const char* tv = getenv("PIR_MP_TW");
+    if (L.p2 <= 8 && !(tv && atoi(tv) == 8)) {
+      PIR_QMP(4, kFusedThreads);
+      return hipGetLastError();
+    }
+  }
   PIR_QMP(kFusedTW, kFusedThreads);
 #undef PIR_QMP
   return hipGetLastError();
