@@ -29,6 +29,17 @@ class PirConfig(ctypes.Structure):
     ]
 
 
+class PirCommInfo(ctypes.Structure):  # pir_comm_info_t (include/pir_engine.h)
+    _fields_ = [
+        ("attached", ctypes.c_int),
+        ("count", ctypes.c_int),
+        ("user_rank", ctypes.c_int),
+        ("device", ctypes.c_int),
+        ("engine_device", ctypes.c_int),
+        ("pci_bus_id", ctypes.c_char * 64),
+    ]
+
+
 class PirKernelTime(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 32), ("ms", ctypes.c_float)]
 
@@ -72,6 +83,9 @@ PROTOTYPES = {
     "pir_engine_num_rows": (_U64, [_P]),
     "pir_engine_set_shard": (_I, [_P, _P, _U64, _U64, _U64]),
     "pir_engine_set_shard_rows": (_I, [_P, _P, _U64, _U64]),
+    "pir_engine_get_shard_rows": (_I, [_P, _P, _U64, _U64]),
+    "pir_engine_encode_across_rows": (_I, [_P, _P, _U64, _I]),
+    "pir_engine_encode_within_rows": (_I, [_P, _P, _U64, ctypes.c_uint32, _I, _I]),
     "pir_engine_fill_shard_random": (_I, [_P, _U64]),
     "pir_engine_encode_across_dev": (_I, [_P, _P, _U64, _U64, _I]),
     "pir_engine_encode_within_dev": (_I, [_P, _P, _U64, _U64, ctypes.c_uint32, _I, _I]),
@@ -114,6 +128,7 @@ PROTOTYPES = {
     "pir_comm_unique_id": (_I, [_P]),
     "pir_comm_attach": (_I, [_P, _P, _I, _I]),
     "pir_comm_detach": (_I, [_P]),
+    "pir_comm_info": (_I, [_P, ctypes.POINTER(PirCommInfo)]),
     # pir_client.h
     "pir_gen_keys": (_I, [_I, _I, _U64, _P, _I, _I, _P, _P]),
     "pir_final_cw": (None, [_I, _I, _I, _P]),
@@ -194,6 +209,7 @@ PROTOTYPES = {
     "assembleWoodruffResponses": (None, [ctypes.POINTER(CClient), _P, _P, _P, _P]),
     "pirSetDevice": (None, [_I]),
     "pirServerShardChanged": (None, [ctypes.POINTER(CServer)]),
+    "pirServerSyncRows": (None, [ctypes.POINTER(CServer)]),
     "pirRunTreeQueryThreads": (None, [ctypes.POINTER(CServer), ctypes.c_void_p, ctypes.c_int,
                                       ctypes.c_void_p]),
     "pirServerSetRows": (None, [ctypes.POINTER(CServer), ctypes.c_void_p, ctypes.c_uint64,

@@ -22,8 +22,44 @@
 
 namespace pir {
 
-// Each translation unit that includes this header owns its own copy of the table.
-static __constant__ uint32_t c_te0[256];
+// Te0[x] = {2 S(x), S(x), S(x), 3 S(x)} (bytes 0-3), S = the AES S-box: affine(x^-1) over
+// GF(2^8)/0x11b (FIPS-197 5.1.1), computed at compile time.  Each translation unit that includes
+// this header owns its own statically initialised copy (nothing to upload at engine creation).
+struct Te0Table {
+  uint32_t v[256];
+};
+constexpr uint8_t aes_xtime_c(uint8_t x) { return (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1b : 0)); }
+constexpr uint8_t aes_mul_c(uint8_t a, uint8_t b) {
+  uint8_t r = 0;
+  while (b) {
+    if (b & 1) r ^= a;
+    a = aes_xtime_c(a);
+    b >>= 1;
+  }
+  return r;
+}
+constexpr Te0Table make_te0() {
+  Te0Table t{};
+  for (int x = 0; x < 256; ++x) {
+    uint8_t inv = 0;
+    if (x) {
+      uint8_t r = 1, b = (uint8_t)x;
+      for (int e = 254; e; e >>= 1) {
+        if (e & 1) r = aes_mul_c(r, b);
+        b = aes_mul_c(b, b);
+      }
+      inv = r;
+    }
+    uint8_t sb = inv;
+    for (int k = 1; k <= 4; ++k) sb ^= (uint8_t)((inv << k) | (inv >> (8 - k)));
+    sb ^= 0x63;
+    t.v[x] = (uint32_t)aes_mul_c(sb, 2) | ((uint32_t)sb << 8) | ((uint32_t)sb << 16) |
+             ((uint32_t)aes_mul_c(sb, 3) << 24);
+  }
+  return t;
+}
+static_assert(make_te0().v[0] == 0xa56363c6u && make_te0().v[1] == 0x847c7cf8u, "AES Te0");
+static __constant__ Te0Table c_te0 = make_te0();
 
 constexpr uint32_t kTeBytes = 256 * 32 * 4;  // one replicated table: 32 KiB
 constexpr uint32_t kTablesBytes = 2 * kTeBytes;
@@ -61,7 +97,7 @@ struct Tab {
 // fill the interleaved table (all threads of the block)
 __device__ __forceinline__ void load_tables(uint32_t* lds) {
   for (int i = threadIdx.x; i < 256 * 64; i += blockDim.x) {
-    const uint32_t v = c_te0[i >> 6];
+    const uint32_t v = c_te0.v[i >> 6];
     lds[i] = (i & 32) ? __builtin_amdgcn_alignbit(v, v, 16) : v;
   }
 }
@@ -75,7 +111,7 @@ __device__ __forceinline__ void load_tables_n(uint32_t* lds) {
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const uint32_t e = wv + k * (NT / 64);
-    v[k] = e < 256 ? c_te0[e] : 0u;
+    v[k] = e < 256 ? c_te0.v[e] : 0u;
   }
   const bool hi = threadIdx.x & 32;
 #pragma unroll
@@ -335,42 +371,6 @@ __device__ __forceinline__ uint32_t aes_col(const Tab& T, uint32_t kq, uint32_t 
       w = last_col(T, w, b, c, d, kq);
   }
   return w;
-}
-
-// ------------------------------------------------------------------------------------------
-// host: Te0 generation + upload into this translation unit's __constant__ copy
-// ------------------------------------------------------------------------------------------
-static inline uint8_t aes_xtime_h(uint8_t x) { return (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1b : 0)); }
-static inline uint8_t aes_mul_h(uint8_t a, uint8_t b) {
-  uint8_t r = 0;
-  while (b) {
-    if (b & 1) r ^= a;
-    a = aes_xtime_h(a);
-    b >>= 1;
-  }
-  return r;
-}
-
-static inline void upload_te0(hipStream_t s) {
-  uint32_t te0[256];
-  for (int x = 0; x < 256; ++x) {  // S-box = affine(x^-1) over GF(2^8)/0x11b (FIPS-197 5.1.1)
-    uint8_t inv = 0;
-    if (x) {
-      uint8_t r = 1, b = (uint8_t)x;
-      for (int e = 254; e; e >>= 1) {
-        if (e & 1) r = aes_mul_h(r, b);
-        b = aes_mul_h(b, b);
-      }
-      inv = r;
-    }
-    uint8_t sb = inv;
-    for (int k = 1; k <= 4; ++k) sb ^= (uint8_t)((inv << k) | (inv >> (8 - k)));
-    sb ^= 0x63;
-    te0[x] = (uint32_t)aes_mul_h(sb, 2) | ((uint32_t)sb << 8) | ((uint32_t)sb << 16) |
-             ((uint32_t)aes_mul_h(sb, 3) << 24);
-  }
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_te0), te0, sizeof(te0), 0, hipMemcpyHostToDevice, s);
-  (void)hipStreamSynchronize(s);
 }
 
 __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {

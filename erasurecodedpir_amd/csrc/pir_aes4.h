@@ -52,7 +52,7 @@ __device__ __forceinline__ void load_tables4_n(uint32_t* lds) {
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t v[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) v[k] = c_te0[wv + k * (NT / 64)];  // row e = wave-uniform
+  for (int k = 0; k < K; ++k) v[k] = c_te0.v[wv + k * (NT / 64)];  // row e = wave-uniform
   const bool hi = threadIdx.x & 32;
 #pragma unroll
   for (int k = 0; k < K; ++k) {

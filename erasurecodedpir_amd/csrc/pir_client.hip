@@ -133,7 +133,6 @@ int pir_gen_keys(int device, int n, uint64_t index, const uint8_t* fcw, int p, i
   if (hipSetDevice(device) != hipSuccess) return PIR_EHIP;
   hipStream_t s;
   if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return PIR_EHIP;
-  pir::upload_te0(s);
   uint8_t *d_fcw = nullptr, *d_seeds = nullptr, *d_keys = nullptr;
   int rc = PIR_OK;
   if (hipMalloc(&d_fcw, (size_t)nq * (p - 1)) != hipSuccess ||

@@ -940,9 +940,6 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
     if (hipEventCreateWithFlags(&e->ev_cb_ready[i], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_cb_free[i], hipEventDisableTiming) != hipSuccess)
       return cleanup(fail(PIR_EHIP, "hipEventCreate failed"));
-  pir::upload_aes_table(e->stream);
-  pir::upload_mp_aes_table(e->stream);
-  pir::upload_leaves_aes_table(e->stream);
   const size_t shard_bytes = (size_t)e->rows * e->pitch;
   if (hipMalloc(&e->d_shard, shard_bytes) != hipSuccess)
     return cleanup(fail(PIR_ENOMEM, "hipMalloc shard %zu bytes", shard_bytes));
@@ -1042,20 +1039,142 @@ int pir_engine_set_shard(pir_engine_t* e, const uint8_t* host, uint64_t row0, ui
   return PIR_OK;
 }
 
+extern "C++" {
+namespace {
+
+// Host threads for the staged row copies below ($PIR_GATHER_THREADS; the GPU box grants 16
+// CPUs per GPU, OMP_NUM_THREADS says how many)
+int gather_threads() {
+  if (const char* v = getenv("PIR_GATHER_THREADS")) return std::max(1, atoi(v));
+  int n = (int)std::thread::hardware_concurrency();
+  if (const char* v = getenv("OMP_NUM_THREADS")) n = std::min(n, std::max(1, atoi(v)));
+  return std::max(1, std::min(8, n));
+}
+
+// fn(t, T) on T host threads (t = 0 on the caller's)
+template <class F>
+void parallel_run(int T, const F& fn) {
+  std::vector<std::thread> th;
+  th.reserve((size_t)T - 1);
+  for (int t = 1; t < T; ++t) th.emplace_back([&fn, t, T] { fn(t, T); });
+  fn(0, T);
+  for (auto& x : th) x.join();
+}
+
+// Host rows -> device through two pinned staging buffers of `chunk_bytes`: chunk c is gathered
+// by T host threads (fill(c, pinned, t, T)) while the DMA and kernel of chunk c - 1 run
+// (issue(c, pinned, stream): its H2D copy and whatever consumes it, enqueued on the engine
+// stream); a pinned buffer is refilled only after the copy that read it has completed.  The
+// pageable single-threaded gather this replaces moved a 16 GiB shard at a few GB/s.
+template <class Fill, class Issue>
+int staged_h2d(pir_engine* e, uint64_t nchunks, size_t chunk_bytes, const Fill& fill,
+               const Issue& issue) {
+  if (!nchunks) return PIR_OK;
+  uint8_t* h[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  const int T = gather_threads();
+  int rc = PIR_OK;
+  for (int i = 0; i < 2 && !rc; ++i) {
+    if (hipHostMalloc(&h[i], chunk_bytes) != hipSuccess ||
+        hipEventCreateWithFlags(&done[i], hipEventDisableTiming) != hipSuccess)
+      rc = fail(PIR_ENOMEM, "pinned staging of %zu bytes", chunk_bytes);
+  }
+  for (uint64_t c = 0; c < nchunks && !rc; ++c) {
+    const int b = (int)(c & 1);
+    if (c >= 2 && hipEventSynchronize(done[b]) != hipSuccess) {
+      rc = fail(PIR_EHIP, "staged upload: chunk %llu", (unsigned long long)(c - 2));
+      break;
+    }
+    parallel_run(T, [&](int t, int nt) { fill(c, h[b], t, nt); });
+    hipError_t err = issue(c, h[b], e->stream);
+    if (err == hipSuccess) err = hipEventRecord(done[b], e->stream);
+    if (err != hipSuccess) rc = fail(PIR_EHIP, "staged upload: %s", hipGetErrorString(err));
+  }
+  if (hipStreamSynchronize(e->stream) != hipSuccess && !rc) rc = fail(PIR_EHIP, "staged upload sync");
+  for (int i = 0; i < 2; ++i) {
+    if (h[i]) (void)hipHostFree(h[i]);
+    if (done[i]) (void)hipEventDestroy(done[i]);
+  }
+  return rc;
+}
+
+// rows per staging chunk: ~64 MiB of `bytes_per_row`
+uint64_t chunk_rows_for(uint64_t bytes_per_row) {
+  return std::max<uint64_t>(1, (64ull << 20) / std::max<uint64_t>(1, bytes_per_row));
+}
+
+}  // namespace
+}  // extern "C++"
+
 int pir_engine_set_shard_rows(pir_engine_t* e, const uint8_t* const* rows, uint64_t row0,
                               uint64_t nrows) {
   if (!e || (!rows && nrows)) return fail(PIR_EINVAL, "null argument");
   if (row0 + nrows > e->rows) return fail(PIR_EINVAL, "rows beyond shard");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
   const uint32_t efs = e->cfg.record_bytes;
-  const uint64_t chunk_rows = std::max<uint64_t>(1, (64ull << 20) / efs);
-  std::vector<uint8_t> stage((size_t)std::min(chunk_rows, nrows) * efs);
-  for (uint64_t r = 0; r < nrows; r += chunk_rows) {
-    const uint64_t m = std::min(chunk_rows, nrows - r);
-    for (uint64_t i = 0; i < m; ++i) memcpy(stage.data() + i * efs, rows[r + i], efs);
-    int rc = pir_engine_set_shard(e, stage.data(), row0 + r, m, efs);
-    if (rc) return rc;
+  const uint64_t m = chunk_rows_for(efs);
+  return staged_h2d(
+      e, (nrows + m - 1) / m, (size_t)m * efs,
+      [&](uint64_t c, uint8_t* dst, int t, int nt) {
+        const uint64_t r0 = c * m, n = std::min(m, nrows - r0);
+        for (uint64_t i = (uint64_t)t; i < n; i += (uint64_t)nt)
+          memcpy(dst + i * efs, rows[r0 + i], efs);
+      },
+      [&](uint64_t c, const uint8_t* src, hipStream_t s) {
+        const uint64_t r0 = c * m, n = std::min(m, nrows - r0);
+        // record_bytes per row; the pad bytes stay zero from the create memset
+        return hipMemcpy2DAsync(e->d_shard + (row0 + r0) * e->pitch, e->pitch, src, efs, efs, n,
+                                hipMemcpyHostToDevice, s);
+      });
+}
+
+int pir_engine_get_shard_rows(pir_engine_t* e, uint8_t* const* rows, uint64_t row0,
+                              uint64_t nrows) {
+  if (!e || (!rows && nrows)) return fail(PIR_EINVAL, "null argument");
+  if (row0 + nrows > e->rows) return fail(PIR_EINVAL, "rows beyond shard");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const uint32_t efs = e->cfg.record_bytes;
+  const uint64_t m = chunk_rows_for(efs), nchunks = (nrows + m - 1) / m;
+  // device -> two pinned buffers (DMA of chunk c + 1 while host threads scatter chunk c)
+  uint8_t* h[2] = {nullptr, nullptr};
+  hipEvent_t ready[2] = {nullptr, nullptr};
+  int rc = PIR_OK;
+  for (int i = 0; i < 2 && !rc; ++i)
+    if (hipHostMalloc(&h[i], (size_t)m * efs) != hipSuccess ||
+        hipEventCreateWithFlags(&ready[i], hipEventDisableTiming) != hipSuccess)
+      rc = fail(PIR_ENOMEM, "pinned staging of %zu bytes", (size_t)m * efs);
+  auto enqueue = [&](uint64_t c) {
+    const uint64_t r0 = c * m, n = std::min(m, nrows - r0);
+    hipError_t err = hipMemcpy2DAsync(h[c & 1], efs, e->d_shard + (row0 + r0) * e->pitch, e->pitch,
+                                      efs, n, hipMemcpyDeviceToHost, e->stream);
+    if (err == hipSuccess) err = hipEventRecord(ready[c & 1], e->stream);
+    return err;
+  };
+  if (!rc && nchunks && enqueue(0) != hipSuccess) rc = fail(PIR_EHIP, "get_shard_rows: copy");
+  const int T = gather_threads();
+  for (uint64_t c = 0; c < nchunks && !rc; ++c) {
+    if (hipEventSynchronize(ready[c & 1]) != hipSuccess) {
+      rc = fail(PIR_EHIP, "get_shard_rows: chunk %llu", (unsigned long long)c);
+      break;
+    }
+    if (c + 1 < nchunks && enqueue(c + 1) != hipSuccess) {
+      rc = fail(PIR_EHIP, "get_shard_rows: copy");
+      break;
+    }
+    const uint64_t r0 = c * m, n = std::min(m, nrows - r0);
+    const uint8_t* src = h[c & 1];
+    parallel_run(T, [&](int t, int nt) {
+      for (uint64_t i = (uint64_t)t; i < n; i += (uint64_t)nt) memcpy(rows[r0 + i], src + i * efs, efs);
+    });
   }
-  return PIR_OK;
+  (void)hipStreamSynchronize(e->stream);
+  for (int i = 0; i < 2; ++i) {
+    if (h[i]) (void)hipHostFree(h[i]);
+    if (ready[i]) (void)hipEventDestroy(ready[i]);
+  }
+  return rc;
 }
 
 int pir_engine_fill_shard_random(pir_engine_t* e, uint64_t seed) {
@@ -1086,6 +1205,102 @@ int pir_engine_encode_across_dev(pir_engine_t* e, const uint8_t* d_files, uint64
                                     e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return PIR_OK;
+}
+
+int pir_engine_encode_across_rows(pir_engine_t* e, const uint8_t* const* files, uint64_t num_files,
+                                  int k) {
+  if (!e || (!files && num_files)) return fail(PIR_EINVAL, "null argument");
+  if (k < 1 || k > 16) return fail(PIR_EINVAL, "k = %d outside [1,16]", k);
+  const uint64_t encdb = (num_files + (uint64_t)k - 1) / (uint64_t)k;
+  if (encdb > (1ull << e->cfg.log_num_records))
+    return fail(PIR_EINVAL, "%llu files over k=%d need %llu rows > 2^%d", (unsigned long long)num_files,
+                k, (unsigned long long)encdb, e->cfg.log_num_records);
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const uint32_t efs = e->cfg.record_bytes;
+  const uint64_t prow0 = (uint64_t)e->cfg.partition_index * e->rows;
+  // chunk c = this engine's rows [c m, (c + 1) m): its k source files per row staged as k blocks
+  // of m rows (block j row r = file encdb j + global row; zero past num_files), so the encode
+  // kernel sees k m "files" of which row r takes m j + r -- the encdb of a k m-file database
+  const uint64_t m = chunk_rows_for((uint64_t)k * efs), nchunks = (e->rows + m - 1) / m;
+  uint8_t* d_stage[2] = {nullptr, nullptr};
+  const size_t sbytes = (size_t)k * m * efs;
+  int rc = PIR_OK;
+  for (int i = 0; i < 2 && !rc; ++i)
+    if (hipMalloc(&d_stage[i], sbytes) != hipSuccess) rc = fail(PIR_ENOMEM, "encode staging");
+  if (!rc)
+    rc = staged_h2d(
+        e, nchunks, sbytes,
+        [&](uint64_t c, uint8_t* dst, int t, int nt) {
+          const uint64_t r0 = c * m, n = std::min(m, e->rows - r0), tot = (uint64_t)k * n;
+          for (uint64_t i = (uint64_t)t; i < tot; i += (uint64_t)nt) {
+            const uint64_t j = i / n, r = i - j * n;
+            const uint64_t src = encdb * j + prow0 + r0 + r;
+            uint8_t* d = dst + (j * n + r) * efs;
+            if (src < num_files) memcpy(d, files[src], efs);
+            else memset(d, 0, efs);
+          }
+        },
+        [&](uint64_t c, const uint8_t* src, hipStream_t s) {
+          const uint64_t r0 = c * m, n = std::min(m, e->rows - r0);
+          uint8_t* ds = d_stage[c & 1];
+          hipError_t err = hipMemcpyAsync(ds, src, (size_t)k * n * efs, hipMemcpyHostToDevice, s);
+          if (err == hipSuccess)
+            err = pir::launch_encode_across(ds, efs, (uint64_t)k * n, k, e->cfg.party_index,
+                                            e->d_shard + r0 * e->pitch, n, 0, e->pitch, efs, s);
+          return err;
+        });
+  for (auto* d : d_stage)
+    if (d) (void)hipFree(d);
+  return rc;
+}
+
+int pir_engine_encode_within_rows(pir_engine_t* e, const uint8_t* const* files, uint64_t num_files,
+                                  uint32_t file_bytes, int k, int party) {
+  if (!e || (!files && num_files)) return fail(PIR_EINVAL, "null argument");
+  if (k < 1 || k > 16) return fail(PIR_EINVAL, "k = %d outside [1,16]", k);
+  if (party < 0 || party > 255) return fail(PIR_EINVAL, "party %d outside [0,255]", party);
+  if ((uint64_t)file_bytes > (uint64_t)k * e->cfg.record_bytes)
+    return fail(PIR_EINVAL, "file_bytes %u > k * record_bytes (%d * %u)", file_bytes, k,
+                e->cfg.record_bytes);
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const uint64_t prow0 = (uint64_t)e->cfg.partition_index * e->rows;
+  const uint32_t fb = std::max<uint32_t>(file_bytes, 1);
+  // chunk c = this engine's rows [c m, (c + 1) m) = files prow0 + c m + r (one file per row)
+  const uint64_t m = chunk_rows_for(fb), nchunks = (e->rows + m - 1) / m;
+  uint8_t* d_stage[2] = {nullptr, nullptr};
+  const size_t sbytes = (size_t)m * fb;
+  int rc = PIR_OK;
+  for (int i = 0; i < 2 && !rc; ++i)
+    if (hipMalloc(&d_stage[i], sbytes) != hipSuccess) rc = fail(PIR_ENOMEM, "encode staging");
+  auto nfiles_of = [&](uint64_t r0, uint64_t n) {
+    const uint64_t g0 = prow0 + r0;
+    return g0 >= num_files ? 0ull : std::min<uint64_t>(n, num_files - g0);
+  };
+  if (!rc)
+    rc = staged_h2d(
+        e, nchunks, sbytes,
+        [&](uint64_t c, uint8_t* dst, int t, int nt) {
+          const uint64_t r0 = c * m, n = std::min(m, e->rows - r0), nf = nfiles_of(r0, n);
+          for (uint64_t i = (uint64_t)t; i < nf; i += (uint64_t)nt)
+            memcpy(dst + i * fb, files[prow0 + r0 + i], file_bytes);
+        },
+        [&](uint64_t c, const uint8_t* src, hipStream_t s) {
+          const uint64_t r0 = c * m, n = std::min(m, e->rows - r0), nf = nfiles_of(r0, n);
+          uint8_t* ds = d_stage[c & 1];
+          hipError_t err = nf ? hipMemcpyAsync(ds, src, (size_t)nf * fb, hipMemcpyHostToDevice, s)
+                              : hipSuccess;
+          if (err == hipSuccess)
+            err = pir::launch_encode_within(ds, fb, nf, file_bytes, k,
+                                            party ? party : e->cfg.party_index,
+                                            e->d_shard + r0 * e->pitch, n, 0, e->pitch,
+                                            e->cfg.record_bytes, s);
+          return err;
+        });
+  for (auto* d : d_stage)
+    if (d) (void)hipFree(d);
+  return rc;
 }
 
 int pir_engine_encode_within_dev(pir_engine_t* e, const uint8_t* d_files, uint64_t file_pitch,
@@ -1585,7 +1800,7 @@ int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, int num_keys, 
   for (int w = 0; w < n; ++w)
     for (int k = 0; k < pir::kQueryTraceSlots; ++k) {
       const uint64_t v = h[(size_t)w * pir::kQueryTraceSlots + k];
-      const bool clk = k == 56 || k == 57 || (k >= 128 && k < 160);  // shader-clock ticks
+      const bool clk = k == 56 || k == 57 || (k >= 128 && k < 160) || k >= 192;  // shader-clock ticks
       out[(size_t)w * pir::kQueryTraceSlots + k] = clk ? v : (v ? v - t0 : 0);
     }
   return nwg;
@@ -1630,6 +1845,22 @@ int pir_comm_detach(pir_engine_t* e) {
   e->comm_failed = false;
   e->nranks = 1;
   e->rank = 0;
+  return PIR_OK;
+}
+
+int pir_comm_info(pir_engine_t* e, pir_comm_info_t* out) {
+  if (!e || !out) return fail(PIR_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  memset(out, 0, sizeof *out);
+  out->attached = e->comm ? 1 : 0;
+  out->count = out->user_rank = out->device = -1;
+  out->engine_device = e->cfg.device;
+  if (e->comm) {
+    RCCL_TRY(ncclCommCount(e->comm, &out->count));
+    RCCL_TRY(ncclCommUserRank(e->comm, &out->user_rank));
+    RCCL_TRY(ncclCommCuDevice(e->comm, &out->device));
+  }
+  HIP_TRY(hipDeviceGetPCIBusId(out->pci_bus_id, (int)sizeof out->pci_bus_id, e->cfg.device));
   return PIR_OK;
 }
 

@@ -56,7 +56,6 @@ TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last = -1, int p
                    int max_front = 16);
 int final_stage_blocks(const TreePlan& pl);  // workgroups of the leaf-converting stage
 
-void upload_aes_table(hipStream_t s);  // Te0 (computed on the host) -> __constant__ memory
 
 hipError_t launch_key_prep(const uint8_t* d_raw, size_t key_stride, int num_keys, int p, int n,
                            int nq, int party0, DevKey* d_keys, hipStream_t s);
@@ -99,7 +98,6 @@ bool leaves_supported(int kd);
 hipError_t launch_leaves(int p, int nrp, int kd, const DevKey* d_key, const uint4* is,
                          const uint32_t* it, int L0, uint64_t nin, int nkeys, uint64_t in_stride,
                          uint8_t* c, uint32_t cstride, uint32_t c_key_off, hipStream_t s);
-void upload_leaves_aes_table(hipStream_t s);
 // The node-writing stages of kd in [1, kNodesMaxK] levels the same way (one input node per
 // lane, its 2^kd descendants of the stage's last level written to os/ot, out_stride per key).
 constexpr int kNodesMaxK = 4;
@@ -174,7 +172,7 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
 inline size_t query_slab_bytes(const QueryPlan& qp) {
   return (size_t)qp.shape.grid.x * qp.shape.grid.y * qp.shape.slab_bytes;
 }
-constexpr int kQueryTraceSlots = 192;  // trace: per-workgroup phase stamps (wall clock, 100 MHz)
+constexpr int kQueryTraceSlots = 256;  // trace: per-workgroup phase stamps (wall clock, 100 MHz)
 // device scratch for the super-tile tile inputs (0 when ls == 0)
 size_t query_scratch_bytes(const QueryPlan& qp);
 // out != nullptr: the answers are reduced in-kernel (no launch_reduce): query k's nq x efs bytes

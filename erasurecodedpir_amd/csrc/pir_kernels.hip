@@ -26,8 +26,6 @@
 
 namespace pir {
 
-void upload_aes_table(hipStream_t s) { upload_te0(s); }
-
 // ------------------------------------------------------------------------------------------
 // k_key_prep: raw key bytes -> DevKey (one workgroup per key)
 // ------------------------------------------------------------------------------------------
@@ -72,11 +70,13 @@ __device__ void parse_key(const uint8_t* __restrict__ key, int p, int n, int nq,
   }
 }
 
+#ifndef PIR_QUERY_PART
 __global__ __launch_bounds__(256) void k_key_prep(const uint8_t* __restrict__ raw,
                                                   size_t key_stride, int p, int n, int nq,
                                                   int party0, DevKey* __restrict__ out) {
   parse_key(raw + blockIdx.x * key_stride, p, n, nq, party0, out + blockIdx.x);
 }
+#endif
 
 
 // ------------------------------------------------------------------------------------------
@@ -114,6 +114,7 @@ __device__ __forceinline__ uint32_t word_of(const uint4& v, uint32_t q) {
   return q == 0 ? v.x : (q == 1 ? v.y : (q == 2 ? v.z : v.w));
 }
 
+#ifndef PIR_QUERY_PART
 __global__ __launch_bounds__(kFrontThreads) void k_frontier(
     const uint8_t* __restrict__ raw, int p, int n, int nq, int party0, DevKey* __restrict__ K,
     uint64_t prefix, int log_parts, int g, int e, uint4* __restrict__ out_s,
@@ -229,6 +230,7 @@ __global__ __launch_bounds__(kFrontThreads) void k_frontier(
     W *= 2;
   }
 }
+#endif  // PIR_QUERY_PART
 
 // ------------------------------------------------------------------------------------------
 // k_expand: the wide, throughput-bound levels.  A workgroup takes `tile` nodes of level L0 and
@@ -420,6 +422,46 @@ __device__ __forceinline__ uint32_t m4r_pack(uint32_t vi, uint32_t sh) {
   t |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x114, 0xf, 0xf, true);  // row_shr:4
   return t;
 }
+// k_query's four-Russians scan waves build the packed indices of a whole tile at once, one
+// group of 4 rows per lane, instead of per group across the wave (8 coefficient readlanes, 7
+// lane-mask ops, a shift, 3 DPP ORs and their wait states per group: profiles/r05/fold_phases_*,
+// phase "index").  c[r] = row r's coefficient word (bytes = rounds 0-7, the ring layout);
+// P[a] = m4r_pack's word for round a: bits [4b, 4b + 4) = bit b of the 4 rows' round-a bytes,
+// row r -> bit r of the nibble.  A 4 x 4 byte transpose (v_perm) gathers W_a = byte r of row r
+// (bit 8r + b), then four delta swaps of index bits move bit 8r + b to 4b + r.
+__device__ __forceinline__ uint32_t m4r_bits_4x8(uint32_t x) {
+  auto ds = [](uint32_t v, int d, uint32_t m) {
+    const uint32_t t = (v ^ (v >> d)) & m;
+    return v ^ t ^ (t << d);
+  };
+  x = ds(x, 7, 0x00AA00AAu);   // index bits 0 <-> 3
+  x = ds(x, 14, 0x0000CCCCu);  // 1 <-> 4
+  x = ds(x, 4, 0x00F000F0u);   // 2 <-> 3
+  return ds(x, 8, 0x0000FF00u);  // 3 <-> 4
+}
+template <int NA>
+__device__ __forceinline__ void m4r_tile_index(const uint2 (&c)[4], uint32_t (&P)[NA]) {
+  static_assert(NA >= 1 && NA <= 5, "rounds 0-4 (coefficient word x: 0-3, y: 4)");
+  const uint32_t A = __builtin_amdgcn_perm(c[1].x, c[0].x, 0x05010400u);  // rows 0-1, rounds 0-1
+  const uint32_t B = __builtin_amdgcn_perm(c[3].x, c[2].x, 0x05010400u);  // rows 2-3, rounds 0-1
+  P[0] = m4r_bits_4x8(__builtin_amdgcn_perm(B, A, 0x05040100u));
+  if constexpr (NA > 1) P[1] = m4r_bits_4x8(__builtin_amdgcn_perm(B, A, 0x07060302u));
+  if constexpr (NA > 2) {
+    const uint32_t C = __builtin_amdgcn_perm(c[1].x, c[0].x, 0x07030602u);  // rounds 2-3
+    const uint32_t D = __builtin_amdgcn_perm(c[3].x, c[2].x, 0x07030602u);
+    P[2] = m4r_bits_4x8(__builtin_amdgcn_perm(D, C, 0x05040100u));
+    if constexpr (NA > 3) P[3] = m4r_bits_4x8(__builtin_amdgcn_perm(D, C, 0x07060302u));
+  }
+  if constexpr (NA > 4) {
+    const uint32_t E = __builtin_amdgcn_perm(c[1].y, c[0].y, 0x0c0c0400u);  // round 4
+    const uint32_t F = __builtin_amdgcn_perm(c[3].y, c[2].y, 0x0c0c0400u);
+    P[4] = m4r_bits_4x8(__builtin_amdgcn_perm(F, E, 0x05040100u));
+  }
+}
+// $PIR_M4R_TILEIDX=0 at build time: the per-group index build of rounds 2-4 (A/B diagnostics)
+#ifndef PIR_M4R_TILEIDX
+#define PIR_M4R_TILEIDX 1
+#endif
 template <int VEC, int NA>
 __device__ __forceinline__ void m4r_fold_group(uint32_t (&Z)[NA][8][VEC], const uint32_t* x0,
                                                const uint32_t* x1, const uint32_t* x2,
@@ -482,7 +524,7 @@ constexpr PlaneMasks make_plane_masks() {
     for (int k = 0; k < 8; ++k) t.m[c * 8 + k] = ((c >> k) & 1) ? 0xffffffffu : 0u;
   return t;
 }
-__constant__ PlaneMasks c_planes = make_plane_masks();
+static __constant__ PlaneMasks c_planes = make_plane_masks();
 
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 #ifndef PIR_PLANE_U
@@ -947,6 +989,19 @@ __device__ __forceinline__ void lds_signal(uint32_t* p) {  // one lane per wave
   if ((threadIdx.x & 63) == 0)
     __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// Diagnostic build only (-DPIR_FOLD_STAMPS=1, tools/fold_phases.py): k_query's four-Russians
+// scan waves add the shader cycles of each phase of their loop into per-wave counters, written
+// to trace[kFoldStampBase + 8 sw + k] at the end.  s_memtime + its wait costs ~10 % of a wave's
+// cycles, so the shares, not the totals, are the finding.  The product build has none of this.
+#ifndef PIR_FOLD_STAMPS
+#define PIR_FOLD_STAMPS 0
+#endif
+constexpr int kFoldStampBase = 192;
+__device__ __forceinline__ uint64_t fold_stamp() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  return t;
+}
 // barrier among `nw` waves (not the whole workgroup): generation-counted LDS counter
 __device__ __forceinline__ void group_barrier(uint32_t* ctr, uint32_t& gen, uint32_t nw) {
   lds_signal(ctr);
@@ -1238,6 +1293,7 @@ __device__ __forceinline__ void stage_key(const uint8_t* __restrict__ raw, int p
 // toggle (a, i, j) set of G(s[i][j], mu)[x] ^ cw[j][x]; multiparty_dpf.cpp:590-601, :665-675)
 // into a k_query ring slot ([record][NRP] bytes), by the first nt threads: lpi lanes per CTR
 // block of the tile (16 records) split the row's seeds, then XOR their partials.  TILE | mu.
+// nt >= TILE / 16 is required (one block per thread at most; query_nq_mp static_asserts it).
 template <int TILE, int NRP>
 __device__ __forceinline__ void mp_tile(const Tab& T, const uint8_t* __restrict__ key,
                                         const MpLayout& L, uint64_t rec0, uint8_t* ring, int tt,
@@ -1780,6 +1836,10 @@ __global__ __launch_bounds__(NT) void k_query(
     // past the tile's row groups are masked)
     const uint32_t rpt = ((ngroups + nwg - 1) / nwg + U - 1) / U * U;
     constexpr bool kM4RExact = kM4R && SW == 8 && TILE == 1024 && 128 % U == 0;
+    // the tile's packed indices one group per lane: 8 scan waves, 2 column groups -> 4 row
+    // waves x 64 groups of 4 rows = the 1024 rows of a tile
+    constexpr bool kM4RLane = kM4RExact && PIR_M4R_TILEIDX && NQ <= 5;
+    const bool lane_tile = kM4RLane && rpt <= 256;  // records of 512 B and 1 KiB (gy <= 2)
     const bool scan = wi < nwg && !(trace && trace_flags_noscan);
     __builtin_amdgcn_s_setprio(PIR_SCAN_PRIO);
     const uint8_t* rbase = shard + (uint64_t)chunk * CH;  // + tile_row0(i) rows
@@ -1798,6 +1858,12 @@ __global__ __launch_bounds__(NT) void k_query(
 
     const uint32_t lane_off = chunk < cpr ? chunk * CH : 0u;
     const uint32_t tile_bytes = (uint32_t)TILE * pitch;
+    // the buffer resource of tile g's rows (num_records 0 past the queue's last tile)
+    auto tile_rsrc = [&](uint32_t g) __attribute__((always_inline)) {
+      return __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(shard + tile_row0(g & (ntiles - 1)) * pitch), (short)0,
+          g < total ? (int)tile_bytes : 0, kBufRsrcWord3);
+    };
     auto load_slot = [&](uint32_t g, uint32_t j, Chunk<VEC>& dst) __attribute__((always_inline)) {
       const uint32_t gi = wi + j * nwg;
       if constexpr (UNI) {
@@ -1847,10 +1913,26 @@ __global__ __launch_bounds__(NT) void k_query(
         for (int u = 0; u < U; ++u) load_slot(0, u, x[u]);
       }
     }
+#if PIR_FOLD_STAMPS
+    uint32_t fs[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per-phase cycles of this wave (fold_stamp)
+    uint64_t fs_t = fold_stamp();
+#define PIR_FS(k)                                          \
+  do {                                                     \
+    if constexpr (kM4R) {                                  \
+      const uint64_t t_ = fold_stamp();                    \
+      fs[k] += (uint32_t)(t_ - fs_t);                      \
+      fs_t = t_;                                           \
+    }                                                      \
+  } while (0)
+#else
+#define PIR_FS(k) do {} while (0)
+#endif
     for (uint32_t g = 0; g < total; ++g) {
       const uint32_t i = g % ntiles;
       const uint8_t* ring = sm.ring[g % RING];
+      PIR_FS(6);  // the previous tile's bookkeeping, end-of-query fold and slab
       lds_wait_geq(&sm.ready, g + 1);
+      PIR_FS(0);  // waiting for the tree (tile g's shares)
       if (!UNI && scan) {  // per-lane coefficients: batches of U rows of this tile
         const uint8_t* base = rbase + tile_row0(i) * pitch;
         for (uint32_t g0 = wi; g0 < ngroups; g0 += U * nwg) {
@@ -1870,7 +1952,56 @@ __global__ __launch_bounds__(NT) void k_query(
         }
       }
       if (UNI && scan) {
-        for (uint32_t j0 = 0; j0 < rpt; j0 += U) {
+        if constexpr (kM4RLane) if (lane_tile) {
+          // four Russians, per tile: lane l builds the packed indices of the wave's group l
+          // (slots 4l .. 4l + 3: rows wi + (4l + r) nwg of the tile; rpt / 4 <= 64 groups)
+          uint2 cr[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t j = 4u * lane + (uint32_t)r;
+            const uint4 c = load_coef<NRP>(ring, j < rpt ? wi + j * nwg : 0u);
+            cr[r] = make_uint2(c.x, c.y);
+          }
+          uint32_t P[NQ];
+          m4r_tile_index<NQ>(cr, P);
+          PIR_FS(5);  // the tile's packed indices (one group per lane)
+          // the refills read this tile's rows, then (the last batch) the next tile's: both
+          // buffer resources once per tile, row offsets as running sums (no per-load address
+          // arithmetic beyond one s_add)
+          const uint32_t rstep = nwg * pitch;
+          auto batch = [&](uint32_t j0, __amdgpu_buffer_rsrc_t rs, uint32_t soff)
+              __attribute__((always_inline)) {
+#pragma unroll
+            for (int g4 = 0; g4 < U; g4 += 4) {
+              uint32_t pk[NQ];
+#pragma unroll
+              for (int a = 0; a < NQ; ++a)
+                pk[a] = (uint32_t)__builtin_amdgcn_readlane((int)P[a], (int)((j0 + g4) >> 2));
+#if PIR_FOLD_STAMPS
+              PIR_FS(1);
+              asm volatile("" ::"v"(x[g4].v[0]), "v"(x[g4].v[1]), "v"(x[g4 + 1].v[0]),
+                           "v"(x[g4 + 1].v[1]), "v"(x[g4 + 2].v[0]), "v"(x[g4 + 2].v[1]),
+                           "v"(x[g4 + 3].v[0]), "v"(x[g4 + 3].v[1]));
+              PIR_FS(2);
+              ++fs[7];
+#endif
+              m4r_fold4s<VEC, NQ>(Z, x[g4].v, x[g4 + 1].v, x[g4 + 2].v, x[g4 + 3].v, pk);
+              PIR_FS(3);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                x[g4 + r] = load_chunk_buf<VEC>(rs, lane_off, soff);
+                soff += rstep;
+              }
+              PIR_FS(4);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          };
+          const __amdgpu_buffer_rsrc_t rs_here = tile_rsrc(g), rs_next = tile_rsrc(g + 1);
+          const uint32_t row_off = wi * pitch;  // slot j at row_off + j * rstep
+          for (uint32_t j0 = 0; j0 + U < rpt; j0 += U) batch(j0, rs_here, row_off + (j0 + U) * rstep);
+          batch(rpt - U, rs_next, row_off);  // refills from the next tile (of this or the next query)
+        }
+        for (uint32_t j0 = 0; j0 < (lane_tile ? 0u : rpt); j0 += U) {
           // wave-uniform coefficients: lane u reads row u's (one LDS read), v_readlane broadcasts
           uint4 cf[U];
           const uint32_t gl = wi + (j0 + (lane < (uint32_t)U ? lane : 0u)) * nwg;
@@ -1883,10 +2014,23 @@ __global__ __launch_bounds__(NT) void k_query(
             for (int g4 = 0; g4 < U; g4 += 4) {
               const uint32_t vi = m4r_index(coef_word(c4, g4), coef_word(c4, g4 + 1),
                                             coef_word(c4, g4 + 2), coef_word(c4, g4 + 3));
+#if PIR_FOLD_STAMPS
+              const uint32_t vp = m4r_pack(vi, (lane & 7u) * 4u);
+              PIR_FS(1);  // coefficient words (the ring read at g4 = 0), index, pack
+              asm volatile("" ::"v"(x[g4].v[0]), "v"(x[g4].v[1]), "v"(x[g4 + 1].v[0]),
+                           "v"(x[g4 + 1].v[1]), "v"(x[g4 + 2].v[0]), "v"(x[g4 + 2].v[1]),
+                           "v"(x[g4 + 3].v[0]), "v"(x[g4 + 3].v[1]));
+              PIR_FS(2);  // the group's rows (s_waitcnt vmcnt)
+              m4r_fold4p<VEC, NQ>(Z, x[g4].v, x[g4 + 1].v, x[g4 + 2].v, x[g4 + 3].v, vp);
+              PIR_FS(3);  // combinations + 40 indexed planes
+              ++fs[7];
+#else
               m4r_fold_group<VEC, NQ>(Z, x[g4].v, x[g4 + 1].v, x[g4 + 2].v, x[g4 + 3].v, vi,
                                       (lane & 7u) * 4u);
+#endif
 #pragma unroll
               for (int r = 0; r < 4; ++r) load_slot(gn, jn + g4 + r, x[g4 + r]);
+              PIR_FS(4);  // the 4 refill loads
               __builtin_amdgcn_sched_barrier(0);
             }
             continue;
@@ -2027,9 +2171,178 @@ __global__ __launch_bounds__(NT) void k_query(
         if (trace && qy == 0 && sw == 0 && lane == 0) trace[6] = wall_clock64();
       }
     }
+#if PIR_FOLD_STAMPS
+    PIR_FS(6);
+    if constexpr (kM4R) {
+      static_assert(kFoldStampBase + 64 <= kQueryTraceSlots, "fold stamps: trace slots");
+      if (trace && lane == 0 && sw < 8)  // the first 8 scan waves
+        for (int k = 0; k < 8; ++k) trace[kFoldStampBase + 8 * sw + k] = fs[k];
+    }
+#endif
+#undef PIR_FS
   }
 }
 
+// ---- fused leaf stage + scan -----------------------------------------------------------------
+constexpr int kFusedTW = 8;       // tree waves per workgroup (the other 8 scan)
+constexpr int kQueryTreeHeavyTW = 12;  // k_query for small records: 12 tree + 4 scan waves
+constexpr int kLoneTile = 1024;        // leaves per tile of a lone query (nk == 1) of large records
+constexpr int kFusedTileIn = 64;  // tree nodes entering a tile
+
+template <int NQ, int TILE>
+hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
+                           int p, int n, int party0, int log_parts, uint64_t prefix,
+                           const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
+                           uint64_t* trace, uint8_t* out, uint32_t* qcnt, uint32_t efs,
+                           uint32_t red_mode) {
+  uint4* fr_s = reinterpret_cast<uint4*>(scratch);
+  uint32_t* fr_t = reinterpret_cast<uint32_t*>(scratch + ((size_t)qp.shape.grid.x << (kQueryKin + qp.ls)) * sizeof(uint4));
+  constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : 8));
+  constexpr int VEC = NQ <= 2 ? 4 : 2;
+  constexpr int RING = TILE == 4096 ? 2 : 4;  // share slots: the tree runs RING-1 tiles ahead
+  const ScanShape& sh = qp.shape;
+#define PIR_QLN(UNI, TW, GY, gy, NTH)                                                            \
+  hipLaunchKernelGGL((k_query<NQ, NRP, VEC, UNI, TW, TILE, GY, RING, NTH>), dim3(sh.grid.x),     \
+                     dim3(NTH), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,                    \
+                     log_parts, prefix, qp.lr, qp.lt, qp.ls, fr_s, fr_t, shard, sh.pitch, sh.cpr,  \
+                     gy, slabs, trace, out, qcnt, efs, red_mode, MpLayout{})
+#define PIR_QL(UNI, TW, GY, gy) PIR_QLN(UNI, TW, GY, gy, kFusedThreads)
+  if constexpr (VEC == 2 && NQ >= 3 && NQ <= 5 && NQ > PIR_QUERY_BRANCH_MAXNQ && TILE == 1024) {
+    if (sh.uniform && qp.m4r) {  // four-Russians scan waves (k_query's kM4R)
+      if (qp.m4r == 2) PIR_QLN(true, 2, 4, sh.grid.y, kM4rThreads);  // diagnostics: 2 tree waves
+      else PIR_QLN(true, kM4rTW, 4, sh.grid.y, kM4rThreads);
+      return hipGetLastError();
+    }
+  }
+  if constexpr (NQ <= 2) {
+    if (qp.tw == kQueryTreeHeavyTW) {  // small records: the tree is the bottleneck
+      if (sh.uniform) PIR_QL(true, kQueryTreeHeavyTW, 4, sh.grid.y);
+      else PIR_QL(false, kQueryTreeHeavyTW, 1, 1u);
+      return hipGetLastError();
+    }
+  }
+  if (sh.uniform) PIR_QL(true, kFusedTW, 4, sh.grid.y);
+  else PIR_QL(false, kFusedTW, 1, 1u);
+#undef PIR_QL
+#undef PIR_QLN
+  return hipGetLastError();
+}
+
+// k_query in its sqrt(N) DPF mode (MPK): mp_tile builds each tile's shares from the key
+template <int NQ, int TILE>
+hipError_t query_nq_mp(const QueryPlan& qp, const uint8_t* d_key, uint32_t key_stride,
+                              int nk, const MpLayout& L, int n, int log_parts, uint64_t prefix,
+                              const uint8_t* shard, uint8_t* slabs, hipStream_t s) {
+  constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : 8));
+  constexpr int VEC = NQ <= 2 ? 4 : 2;
+  constexpr int RING = TILE == 4096 ? 2 : 4;
+  const ScanShape& sh = qp.shape;
+  if (!sh.uniform) return hipErrorInvalidValue;
+  // tree-wave priority as launch_query (a lone query's share waves at 3)
+  const char* tp = getenv("PIR_QUERY_TREE_PRIO");
+  const uint32_t rm = ((tp ? (uint32_t)atoi(tp) : (nk == 1 ? 3u : 0u)) & 3u) << 8;
+  // mp_tile gives each of its threads at most ONE 16-record CTR block of the tile (no loop
+  // over blocks): the share waves (TW * 64 threads; tile 0: all NTH) must cover TILE / 16 blocks
+#define PIR_QMP(TW, NTH)                                                                         \
+  static_assert((TW) * 64 >= TILE / 16, "mp_tile: one thread per CTR block of the tile");      \
+  hipLaunchKernelGGL((k_query<NQ, NRP, VEC, true, TW, TILE, 4, RING, NTH, true>),               \
+                     dim3(sh.grid.x), dim3(NTH), 0, s, d_key, key_stride, nk, 2, n, NQ, 0,       \
+                     log_parts, prefix, qp.lr, qp.lt, 0, nullptr, nullptr, shard, sh.pitch,      \
+                     sh.cpr, sh.grid.y, slabs, nullptr, nullptr, nullptr, 0u, rm, L)
+  if constexpr (VEC == 2 && NQ >= 3 && NQ <= 5 && NQ > PIR_QUERY_BRANCH_MAXNQ && TILE == 1024) {
+    if (qp.m4r) {
+      PIR_QMP(kM4rTW, kM4rThreads);
+      return hipGetLastError();
+    }
+  }
+  // 1-2 shares: few seeds per row (p2 <= 8) build a tile's shares in a fraction of the scan's
+  // time, so 4 share waves + 12 scan waves ($PIR_MP_TW=8: the tree DPF's 8 + 8)
+  if constexpr (NQ <= 2) {
+    const char* tv = getenv("PIR_MP_TW");
+    if (L.p2 <= 8 && !(tv && atoi(tv) == 8)) {
+      PIR_QMP(4, kFusedThreads);
+      return hipGetLastError();
+    }
+  }
+  PIR_QMP(kFusedTW, kFusedThreads);
+#undef PIR_QMP
+  return hipGetLastError();
+}
+
+// ---- where the k_query instantiations are compiled ---------------------------------------
+// Every (rounds, tile) instance of query_nq / query_nq_mp (each a few k_query kernels) is
+// compiled in one of kQueryParts objects: this file built again with -DPIR_QUERY_PART=k (the
+// Makefile's pir_query_k.o), which keeps only the templates and the instances of part k, so the
+// parts compile in parallel.  The main object declares them extern.
+#define PIR_QNQ_ARGS                                                                            \
+  (const QueryPlan&, const uint8_t*, uint32_t, int, int, int, int, int, uint64_t, const uint8_t*, \
+   uint8_t*, uint8_t*, hipStream_t, uint64_t*, uint8_t*, uint32_t*, uint32_t, uint32_t)
+#define PIR_QMP_ARGS                                                                            \
+  (const QueryPlan&, const uint8_t*, uint32_t, int, const MpLayout&, int, int, uint64_t,         \
+   const uint8_t*, uint8_t*, hipStream_t)
+// X(function, rounds, tile, part)
+#define PIR_QUERY_INSTANCES(X)                                                                   \
+  X(query_nq, 5, 1024, 0) X(query_nq, 4, 1024, 1) X(query_nq, 3, 1024, 2)                        \
+  X(query_nq, 1, 4096, 3) X(query_nq, 2, 4096, 3) X(query_nq, 1, 1024, 4) X(query_nq, 2, 1024, 4) \
+  X(query_nq, 1, 512, 5) X(query_nq, 2, 512, 5) X(query_nq, 1, 256, 5) X(query_nq, 2, 256, 5)     \
+  X(query_nq, 6, 1024, 6) X(query_nq, 7, 1024, 6) X(query_nq, 8, 1024, 6)                        \
+  X(query_nq_mp, 1, 4096, 7) X(query_nq_mp, 2, 4096, 7) X(query_nq_mp, 1, 1024, 7)               \
+  X(query_nq_mp, 2, 1024, 7) X(query_nq_mp, 3, 1024, 2) X(query_nq_mp, 4, 1024, 1)              \
+  X(query_nq_mp, 5, 1024, 0)
+constexpr int kQueryParts = 8;
+#define PIR_ARGS_query_nq PIR_QNQ_ARGS
+#define PIR_ARGS_query_nq_mp PIR_QMP_ARGS
+#ifdef PIR_QUERY_PART
+static_assert(PIR_QUERY_PART >= 0 && PIR_QUERY_PART < kQueryParts, "PIR_QUERY_PART");
+#define PIR_QI(F, NQ, TL, PART) \
+  PIR_QI_##PART(template hipError_t F<NQ, TL> PIR_ARGS_##F;)
+#else
+#define PIR_QI(F, NQ, TL, PART) extern template hipError_t F<NQ, TL> PIR_ARGS_##F;
+#endif
+#if defined(PIR_QUERY_PART) && PIR_QUERY_PART == 0
+#define PIR_QI_0(...) __VA_ARGS__
+#else
+#define PIR_QI_0(...)
+#endif
+#if defined(PIR_QUERY_PART) && PIR_QUERY_PART == 1
+#define PIR_QI_1(...) __VA_ARGS__
+#else
+#define PIR_QI_1(...)
+#endif
+#if defined(PIR_QUERY_PART) && PIR_QUERY_PART == 2
+#define PIR_QI_2(...) __VA_ARGS__
+#else
+#define PIR_QI_2(...)
+#endif
+#if defined(PIR_QUERY_PART) && PIR_QUERY_PART == 3
+#define PIR_QI_3(...) __VA_ARGS__
+#else
+#define PIR_QI_3(...)
+#endif
+#if defined(PIR_QUERY_PART) && PIR_QUERY_PART == 4
+#define PIR_QI_4(...) __VA_ARGS__
+#else
+#define PIR_QI_4(...)
+#endif
+#if defined(PIR_QUERY_PART) && PIR_QUERY_PART == 5
+#define PIR_QI_5(...) __VA_ARGS__
+#else
+#define PIR_QI_5(...)
+#endif
+#if defined(PIR_QUERY_PART) && PIR_QUERY_PART == 6
+#define PIR_QI_6(...) __VA_ARGS__
+#else
+#define PIR_QI_6(...)
+#endif
+#if defined(PIR_QUERY_PART) && PIR_QUERY_PART == 7
+#define PIR_QI_7(...) __VA_ARGS__
+#else
+#define PIR_QI_7(...)
+#endif
+PIR_QUERY_INSTANCES(PIR_QI)
+#undef PIR_QI
+
+#ifndef PIR_QUERY_PART  // the rest: the main object only
 // slabs: [grid.y][gx_all][nq][GW words]; out[a*efs + b] for b < efs.
 // One 1024-thread block per 64 output words: 16 lane groups split the gx slabs, then LDS.
 // blockIdx.y = query of a queue: slabs q_words apart, answers gridDim.z*nq*efs bytes apart.
@@ -2252,12 +2565,6 @@ TreePlan make_plan(int n, int log_parts, uint64_t prefix, int k_last, int p, int
   return pl;
 }
 
-// ---- fused leaf stage + scan -----------------------------------------------------------------
-constexpr int kFusedTW = 8;       // tree waves per workgroup (the other 8 scan)
-constexpr int kQueryTreeHeavyTW = 12;  // k_query for small records: 12 tree + 4 scan waves
-constexpr int kLoneTile = 1024;        // leaves per tile of a lone query (nk == 1) of large records
-constexpr int kFusedTileIn = 64;  // tree nodes entering a tile
-
 int fused_tile(int nq, uint32_t pitch, uint64_t nleaves, int num_cus) {
   if (nq > 8) return 0;
   const int vec = nq <= 2 ? 4 : 2;
@@ -2399,83 +2706,6 @@ QueryPlan make_query_plan(int n, int log_parts, int p, int nq, uint32_t pitch, i
   return qp;
 }
 
-template <int NQ, int TILE>
-static hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
-                           int p, int n, int party0, int log_parts, uint64_t prefix,
-                           const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
-                           uint64_t* trace, uint8_t* out, uint32_t* qcnt, uint32_t efs,
-                           uint32_t red_mode) {
-  uint4* fr_s = reinterpret_cast<uint4*>(scratch);
-  uint32_t* fr_t = reinterpret_cast<uint32_t*>(scratch + ((size_t)qp.shape.grid.x << (kQueryKin + qp.ls)) * sizeof(uint4));
-  constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : 8));
-  constexpr int VEC = NQ <= 2 ? 4 : 2;
-  constexpr int RING = TILE == 4096 ? 2 : 4;  // share slots: the tree runs RING-1 tiles ahead
-  const ScanShape& sh = qp.shape;
-#define PIR_QLN(UNI, TW, GY, gy, NTH)                                                            \
-  hipLaunchKernelGGL((k_query<NQ, NRP, VEC, UNI, TW, TILE, GY, RING, NTH>), dim3(sh.grid.x),     \
-                     dim3(NTH), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,                    \
-                     log_parts, prefix, qp.lr, qp.lt, qp.ls, fr_s, fr_t, shard, sh.pitch, sh.cpr,  \
-                     gy, slabs, trace, out, qcnt, efs, red_mode, MpLayout{})
-#define PIR_QL(UNI, TW, GY, gy) PIR_QLN(UNI, TW, GY, gy, kFusedThreads)
-  if constexpr (VEC == 2 && NQ >= 3 && NQ <= 5 && NQ > PIR_QUERY_BRANCH_MAXNQ && TILE == 1024) {
-    if (sh.uniform && qp.m4r) {  // four-Russians scan waves (k_query's kM4R)
-      if (qp.m4r == 2) PIR_QLN(true, 2, 4, sh.grid.y, kM4rThreads);  // diagnostics: 2 tree waves
-      else PIR_QLN(true, kM4rTW, 4, sh.grid.y, kM4rThreads);
-      return hipGetLastError();
-    }
-  }
-  if constexpr (NQ <= 2) {
-    if (qp.tw == kQueryTreeHeavyTW) {  // small records: the tree is the bottleneck
-      if (sh.uniform) PIR_QL(true, kQueryTreeHeavyTW, 4, sh.grid.y);
-      else PIR_QL(false, kQueryTreeHeavyTW, 1, 1u);
-      return hipGetLastError();
-    }
-  }
-  if (sh.uniform) PIR_QL(true, kFusedTW, 4, sh.grid.y);
-  else PIR_QL(false, kFusedTW, 1, 1u);
-#undef PIR_QL
-#undef PIR_QLN
-  return hipGetLastError();
-}
-
-// k_query in its sqrt(N) DPF mode (MPK): mp_tile builds each tile's shares from the key
-template <int NQ, int TILE>
-static hipError_t query_nq_mp(const QueryPlan& qp, const uint8_t* d_key, uint32_t key_stride,
-                              int nk, const MpLayout& L, int n, int log_parts, uint64_t prefix,
-                              const uint8_t* shard, uint8_t* slabs, hipStream_t s) {
-  constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : 8));
-  constexpr int VEC = NQ <= 2 ? 4 : 2;
-  constexpr int RING = TILE == 4096 ? 2 : 4;
-  const ScanShape& sh = qp.shape;
-  if (!sh.uniform) return hipErrorInvalidValue;
-  // tree-wave priority as launch_query (a lone query's share waves at 3)
-  const char* tp = getenv("PIR_QUERY_TREE_PRIO");
-  const uint32_t rm = ((tp ? (uint32_t)atoi(tp) : (nk == 1 ? 3u : 0u)) & 3u) << 8;
-#define PIR_QMP(TW, NTH)                                                                         \
-  hipLaunchKernelGGL((k_query<NQ, NRP, VEC, true, TW, TILE, 4, RING, NTH, true>),               \
-                     dim3(sh.grid.x), dim3(NTH), 0, s, d_key, key_stride, nk, 2, n, NQ, 0,       \
-                     log_parts, prefix, qp.lr, qp.lt, 0, nullptr, nullptr, shard, sh.pitch,      \
-                     sh.cpr, sh.grid.y, slabs, nullptr, nullptr, nullptr, 0u, rm, L)
-  if constexpr (VEC == 2 && NQ >= 3 && NQ <= 5 && NQ > PIR_QUERY_BRANCH_MAXNQ && TILE == 1024) {
-    if (qp.m4r) {
-      PIR_QMP(kM4rTW, kM4rThreads);
-      return hipGetLastError();
-    }
-  }
-  // 1-2 shares: few seeds per row (p2 <= 8) build a tile's shares in a fraction of the scan's
-  // time, so 4 share waves + 12 scan waves ($PIR_MP_TW=8: the tree DPF's 8 + 8)
-  if constexpr (NQ <= 2) {
-    const char* tv = getenv("PIR_MP_TW");
-    if (L.p2 <= 8 && !(tv && atoi(tv) == 8)) {
-      PIR_QMP(4, kFusedThreads);
-      return hipGetLastError();
-    }
-  }
-  PIR_QMP(kFusedTW, kFusedThreads);
-#undef PIR_QMP
-  return hipGetLastError();
-}
-
 hipError_t launch_query_mp(const QueryPlan& qp, const uint8_t* d_key, uint32_t key_stride,
                            int nk, const MpLayout& L, int n, int log_parts, uint64_t prefix,
                            const uint8_t* shard, uint8_t* slabs, hipStream_t s) {
@@ -2519,9 +2749,13 @@ hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_
   // prio 3 for a lone query's tree waves, the default 0 in a queue (same box, configs[1] lone
   // 0.2500 -> 0.2423 ms; a 2^24 x 1 KiB queue 2.55 -> 2.68 ms at prio 3:
   // profiles/r04/bench_tree_prio.jsonl)
+  // Round 5: the four-Russians k_query (3-5 rounds) is paced by its 4 tree waves even in a
+  // queue -- its scan waves spent 28 % of their cycles waiting for shares at prio 0
+  // (profiles/r05/fold_phases_c5_prio0.txt) -- so its tree waves run at 3 there too (configs[4]
+  // queue 3.741 -> 3.488 ms per query, same box: profiles/r05/r5b_c5_tree_prio.jsonl)
   {
     const char* tp = getenv("PIR_QUERY_TREE_PRIO");
-    red_mode |= ((tp ? (uint32_t)atoi(tp) : (nk == 1 ? 3u : 0u)) & 3u) << 8;
+    red_mode |= ((tp ? (uint32_t)atoi(tp) : ((nk == 1 || qp.m4r) ? 3u : 0u)) & 3u) << 8;
   }
 #define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, scratch, s, trace, out, qcnt, efs, red_mode)
 #ifdef PIR_DEV_NQ  // development builds only (ISA / register checks): one round count
@@ -2837,5 +3071,7 @@ hipError_t launch_fill_shard(uint8_t* d_shard, uint64_t rows, uint32_t pitch, ui
                      d_shard, rows, pitch, efs, global_row0, seed);
   return hipGetLastError();
 }
+
+#endif  // !PIR_QUERY_PART
 
 }  // namespace pir

@@ -20,7 +20,6 @@
 
 namespace pir {
 
-void upload_leaves_aes_table(hipStream_t s) { upload_te0(s); }
 
 constexpr int kLeafThreads = 1024;  // one workgroup (128 KiB of tables) per CU: 16 waves
 

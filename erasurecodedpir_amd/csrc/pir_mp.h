@@ -40,6 +40,5 @@ bool cd_layout(int n, int q_needed, int num_cd_keys, MpLayout* out);
 hipError_t launch_mp_shares(const MpLayout& L, const uint8_t* d_key, uint64_t rec_lo,
                             uint64_t rec_hi, int nrp, uint8_t* d_c, int num_cus, hipStream_t s);
 // this translation unit's copy of the AES table (once per device, before the first launch)
-void upload_mp_aes_table(hipStream_t s);
 
 }  // namespace pir

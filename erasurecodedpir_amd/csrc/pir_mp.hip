@@ -17,7 +17,6 @@
 
 namespace pir {
 
-void upload_mp_aes_table(hipStream_t s) { upload_te0(s); }
 
 int mp_choose(int n, int k) { return k == 0 ? 1 : (n * mp_choose(n - 1, k - 1)) / k; }
 

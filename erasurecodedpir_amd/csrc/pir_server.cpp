@@ -8,6 +8,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/random.h>
 
 #include <algorithm>
@@ -91,6 +92,9 @@ struct SliceGroup {
   std::condition_variable cv;
 };
 constexpr size_t kMaxSliceGroups = 8;  // queries whose slices are in flight at once
+// and at most this many bytes of their parts (T x NUM_ROUNDS x EFS each); the oldest group goes
+// first (its remaining callers, if any, still hold it and copy their slices out)
+constexpr size_t kMaxSliceGroupBytes = 256ull << 20;
 
 // Per-server engine state, hung off server.ctx.
 struct ShimState {
@@ -101,9 +105,16 @@ struct ShimState {
   pir_engine_t* eng = nullptr;
   pir_engine_config cfg{};
   bool dirty = true;  // indexList changed since the last upload
+  // the setup encoded the shard on the GPU (encode_*_files_server): the device copy is the only
+  // one and indexList is materialised from it only when something reads or writes the host rows
+  // (sync_rows_down: an engine remake, pirServerSetRows, pirServerSyncRows, a second encode)
+  bool host_stale = false;
+  bool rows_zero = true;  // indexList untouched since initializeServer (all zero)
   uint32_t rows_alloc = 0;
   uint32_t row_bytes = 0;          // bytes per indexList row (initializeServer's fileSizeBytes)
+  uint8_t* row_block = nullptr;    // the rows' one allocation (indexList[i] = row_block + i * row_bytes)
   std::vector<std::shared_ptr<SliceGroup>> groups;  // oldest first
+  size_t group_bytes = 0;          // parts held by `groups`
 };
 
 ShimState* state_of(server* s) {
@@ -119,8 +130,20 @@ ShimState* state_of(server* s) {
   abort();
 }
 
-// Make sure the engine matches the current globals / nq and holds the current indexList.
-pir_engine_t* engine_for(server* s, ShimState* st, int nq) {
+// indexList <- the device shard, when the setup left the device copy as the only one (caller
+// holds st->mu; no slice pass may be running: under the exclusive life lock, or before any)
+void sync_rows_down(server* s, ShimState* st) {
+  if (!st->host_stale || !st->eng) return;
+  const uint64_t n = std::min<uint64_t>(pir_engine_num_rows(st->eng), st->rows_alloc);
+  if (pir_engine_get_shard_rows(st->eng, s->indexList, 0, n) != PIR_OK) die("pirServerSyncRows");
+  st->host_stale = false;
+}
+
+// Make sure the engine matches the current globals / nq and holds the current indexList
+// (upload = false: the caller is about to write the whole device shard itself).
+// must = false: return nullptr instead of aborting when no engine can be created (a setup on a
+// host without a usable GPU keeps the reference's host encode; every query still fails loudly).
+pir_engine_t* engine_for(server* s, ShimState* st, int nq, bool upload = true, bool must = true) {
   pir_engine_config c{};
   c.device = device_default();
   // the party count only sizes DPF keys; polynomial-PIR setups may have p < 2 or > 17
@@ -137,13 +160,24 @@ pir_engine_t* engine_for(server* s, ShimState* st, int nq) {
   if (remake || st->dirty) {  // no slice pass may be using the engine or the shard meanwhile
     excl.lock();
     st->groups.clear();
+    st->group_bytes = 0;
   }
   if (remake) {
+    if (upload) sync_rows_down(s, st);  // the old engine holds the only copy of the shard
     if (st->eng) pir_engine_destroy(st->eng);
     st->eng = nullptr;
-    if (pir_engine_create(&c, &st->eng) != PIR_OK) die("pir_engine_create");
+    if (pir_engine_create(&c, &st->eng) != PIR_OK) {
+      if (must) die("pir_engine_create");
+      st->eng = nullptr;
+      return nullptr;
+    }
     st->cfg = c;
     st->dirty = true;
+    st->host_stale = false;
+  }
+  if (!upload) {
+    st->dirty = false;
+    return st->eng;
   }
   if (st->dirty) {
     const uint64_t n = 1ull << c.log_num_records;
@@ -157,6 +191,52 @@ pir_engine_t* engine_for(server* s, ShimState* st, int nq) {
     st->dirty = false;
   }
   return st->eng;
+}
+
+// Large zeroed host blocks (the client's files, the server's rows): anonymous mappings, so
+// untouched pages cost nothing (a GPU setup never touches the server rows) and huge pages cut
+// the faults of filling tens of GiB.  The sizes live here, keyed by address, for big_free.
+std::mutex g_big_mu;
+std::vector<std::pair<void*, size_t>> g_big;
+uint8_t* big_alloc(size_t bytes) {
+  bytes = std::max<size_t>(bytes, 1);
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) return nullptr;
+  (void)madvise(p, bytes, MADV_HUGEPAGE);
+  std::lock_guard<std::mutex> lk(g_big_mu);
+  g_big.emplace_back(p, bytes);
+  return static_cast<uint8_t*>(p);
+}
+void big_free(void* p) {
+  if (!p) return;
+  size_t bytes = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_big_mu);
+    for (auto it = g_big.begin(); it != g_big.end(); ++it)
+      if (it->first == p) {
+        bytes = it->second;
+        g_big.erase(it);
+        break;
+      }
+  }
+  if (bytes) (void)munmap(p, bytes);
+}
+
+// host threads for the shim's own bulk work (client files); the GPU box grants 16 CPUs per GPU
+int shim_threads() {
+  if (const char* v = getenv("PIR_GATHER_THREADS")) return std::max(1, atoi(v));
+  int n = (int)std::thread::hardware_concurrency();
+  if (const char* v = getenv("OMP_NUM_THREADS")) n = std::min(n, std::max(1, atoi(v)));
+  return std::max(1, std::min(8, n));
+}
+
+// the host encode wrote indexList: the engine re-uploads it before the next query
+void shard_written_on_host(server* s) {
+  if (!s->ctx) return;
+  ShimState* st = static_cast<ShimState*>(s->ctx);
+  std::lock_guard<std::mutex> lk(st->mu);
+  st->rows_zero = false;
+  st->dirty = true;
 }
 
 // The worker threads of pirRunTreeQueryThreads: created once, T of them per fan-out.  A worker
@@ -532,7 +612,22 @@ void assembleHollantiResponses(client* c, uint8_t* erasureIndexList, uint8_t*** 
 void pirSetDevice(int device) { g_device = device; }
 
 void pirServerShardChanged(server* s) {
-  if (s && s->ctx) static_cast<ShimState*>(s->ctx)->dirty = true;
+  if (!s || !s->ctx) return;
+  ShimState* st = static_cast<ShimState*>(s->ctx);
+  std::lock_guard<std::mutex> lk(st->mu);
+  if (st->host_stale)  // the caller wrote rows it never read back (see pir_server.h)
+    fprintf(stderr, "pir shim: indexList written after a GPU setup without pirServerSyncRows; "
+                    "its other rows are zero on the host and now replace the device shard\n");
+  st->host_stale = false;
+  st->rows_zero = false;
+  st->dirty = true;
+}
+
+void pirServerSyncRows(server* s) {
+  ShimState* st = state_of(s);
+  std::lock_guard<std::mutex> lk(st->mu);
+  std::unique_lock<std::shared_mutex> excl(st->life);  // no slice pass reads the shard meanwhile
+  sync_rows_down(s, st);
 }
 
 void pirServerSetRows(server* s, const uint8_t* rows, uint64_t row0, uint64_t nrows,
@@ -545,8 +640,13 @@ void pirServerSetRows(server* s, const uint8_t* rows, uint64_t row0, uint64_t nr
             (unsigned long long)row0, (unsigned long long)(row0 + nrows), st->rows_alloc);
     abort();
   }
+  {
+    std::unique_lock<std::shared_mutex> excl(st->life);
+    sync_rows_down(s, st);  // the rows not written here keep the GPU setup's values
+  }
   for (uint64_t i = 0; i < nrows; ++i)
     memcpy(s->indexList[row0 + i], rows + i * rowBytes, rowBytes);
+  st->rows_zero = false;
   st->dirty = true;
 }
 
@@ -558,8 +658,9 @@ int calcOptimizedDPFTreeKeyLength(int p, int log_domainSize, int numQueries) {
 // setModeParams(CD) sets M to 2 for K = 2, B = 1 (params.cpp:439-441) and a covering-design
 // selection clears isRss (:520-599); the reference never resets either, so a later setup's party
 // count and NUM_RSS_KEYS depend on the process's call history.  This shim starts every
-// setSystemParams from M = 4, isRss = 1, as a fresh process would (the Go servers set their
-// parameters once).
+// setSystemParams from M = 4, isRss = 1 and the CD532 key counts (NUM_CD_KEYS = 2,
+// NUM_CD_KEYS_NEEDED = 4, params.cpp:368-369), as a fresh process would (the Go servers set
+// their parameters once).
 static int g_cd_m = 4;
 
 // The covering designs of params.cpp:519-599: (T, NUM_PARTIES, M) -> NUM_CD_KEYS,
@@ -605,6 +706,8 @@ void setSystemParams(int logNumFiles, int fileSizeBytes, int t, int k, int r, in
   CHECK_MAC = checkMac;
   MODE = mode;
   g_cd_m = 4;
+  NUM_CD_KEYS = 2;  // params.cpp:368-369 (CD532) until select_covering picks a design
+  NUM_CD_KEYS_NEEDED = 4;
   if (mode == 4) {
     if (K == 4 && B == 2) {
       NUM_PARTIES = 16;
@@ -668,19 +771,35 @@ void initializeServer(server* s, int partyIndex, uint32_t logNumFiles, uint32_t 
   s->ctxThreads = nullptr;
   s->partyIndex = partyIndex;
   const uint32_t n = 1u << logNumFiles;
+  // one zeroed allocation for all N rows (the reference mallocs each, server.cpp:34-38): the
+  // pages are only touched when rows are written, not by a GPU setup
   s->indexList = (uint8_t**)malloc((size_t)n * sizeof(uint8_t*));
-  for (uint32_t i = 0; i < n; ++i) s->indexList[i] = (uint8_t*)calloc(fileSizeBytes, 1);
+  st->row_block = big_alloc((size_t)n * fileSizeBytes);
+  if (!s->indexList || !st->row_block) {
+    fprintf(stderr, "pir shim: cannot allocate %u rows of %u bytes\n", n, fileSizeBytes);
+    abort();
+  }
+  for (uint32_t i = 0; i < n; ++i) s->indexList[i] = st->row_block + (size_t)i * fileSizeBytes;
   st->rows_alloc = n;
   s->isByzantine = isByzantine;
   s->numThreads = numThreads;
 }
 
 // server.cpp:45-52
+// No Thread call may start once freeServer has begun (the reference frees the rows under any
+// caller alike); one still inside its slice-group pass is waited for (the life lock).
 void freeServer(server* s) {
   if (!s || !s->ctx) return;
   ShimState* st = static_cast<ShimState*>(s->ctx);
-  if (st->eng) pir_engine_destroy(st->eng);
-  for (uint32_t i = 0; i < st->rows_alloc; ++i) free(s->indexList[i]);
+  {
+    std::lock_guard<std::mutex> lk(st->mu);
+    std::unique_lock<std::shared_mutex> excl(st->life);
+    st->groups.clear();
+    st->group_bytes = 0;
+    if (st->eng) pir_engine_destroy(st->eng);
+    st->eng = nullptr;
+  }
+  big_free(st->row_block);
   free(s->indexList);
   s->indexList = nullptr;
   delete st;
@@ -721,8 +840,10 @@ void runOptimizedDPFTreeQueryThread(server* s, uint8_t* key, int threadNum, int 
         NUM_PARTIES < 2 ? 2 : NUM_PARTIES, LOG_NUM_ENCODED_FILES, NUM_ROUNDS);
     // groups whose every slice was copied out are done
     st->groups.erase(std::remove_if(st->groups.begin(), st->groups.end(),
-                                    [](const std::shared_ptr<SliceGroup>& x) {
-                                      return x->left.load(std::memory_order_acquire) == 0;
+                                    [st](const std::shared_ptr<SliceGroup>& x) {
+                                      const bool done = x->left.load(std::memory_order_acquire) == 0;
+                                      if (done) st->group_bytes -= x->parts.size();
+                                      return done;
                                     }),
                      st->groups.end());
     for (auto& x : st->groups)
@@ -732,7 +853,13 @@ void runOptimizedDPFTreeQueryThread(server* s, uint8_t* key, int threadNum, int 
         break;
       }
     if (!g) {  // the first call of this query: it answers every slice
-      if (st->groups.size() >= kMaxSliceGroups) st->groups.erase(st->groups.begin());
+      const size_t need = (size_t)numThreads * ans;
+      while (!st->groups.empty() && (st->groups.size() >= kMaxSliceGroups ||
+                                     st->group_bytes + need > kMaxSliceGroupBytes)) {
+        st->group_bytes -= st->groups.front()->parts.size();
+        st->groups.erase(st->groups.begin());
+      }
+      st->group_bytes += need;
       g = std::make_shared<SliceGroup>();
       g->key.assign(key, key + klen);
       g->num_threads = numThreads;
@@ -938,34 +1065,85 @@ void runWoodruffQueryThread(server*, uint8_t*, int, int, int, uint8_t**) {
   out_of_scope("runWoodruffQueryThread", "Woodruff");
 }
 
-// client.cpp:16-33 (synthetic DB; MAC tags are outside this engine's scope)
+// client.cpp:16-33 (synthetic DB; MAC tags are outside this engine's scope).  The files share
+// one allocation (held in c->ctx, which the reference uses for an unused EVP context) and are
+// filled by host threads: the reference's per-file malloc + memset of NUM_FILES rows is most of
+// a large setup's host time (2^26 x 1 KiB for configs[4]'s k = 5).
 void initialize_client(client* c, uint8_t log_num_files, uint32_t file_size_bytes) {
   (void)file_size_bytes;
   if (CHECK_MAC) {
     fprintf(stderr, "pir shim: CHECK_MAC setups are outside the engine's scope\n");
     abort();
   }
-  c->ctx = nullptr;
   c->macCtx = nullptr;
   c->macKey = (uint8_t*)"1234567812345678";
-  const uint32_t n = 1u << log_num_files;
+  const uint64_t n = 1ull << log_num_files, fb = FILE_SIZE_BYTES;
   c->unencoded_files = (uint8_t**)malloc((size_t)n * sizeof(uint8_t*));
-  for (uint32_t i = 0; i < n; ++i) {
-    c->unencoded_files[i] = (uint8_t*)malloc(FILE_SIZE_BYTES);
-    memset(c->unencoded_files[i], (int)(i & 0xff), PAYLOAD_SIZE_BYTES);
-    if (i == 1)
-      for (uint32_t j = 0; j < PAYLOAD_SIZE_BYTES; ++j) c->unencoded_files[i][j] = (uint8_t)j;
+  uint8_t* block = big_alloc((size_t)(n * fb));
+  if (!c->unencoded_files || !block) {
+    fprintf(stderr, "pir shim: cannot allocate %llu client files of %llu bytes\n",
+            (unsigned long long)n, (unsigned long long)fb);
+    abort();
   }
+  c->ctx = block;
+  const uint32_t pb = PAYLOAD_SIZE_BYTES;
+  const int T = shim_threads();
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([=] {
+      for (uint64_t i = (uint64_t)t; i < n; i += (uint64_t)T) {
+        uint8_t* f = block + i * fb;
+        c->unencoded_files[i] = f;
+        memset(f, (int)(i & 0xff), pb);
+        if (fb > pb) memset(f + pb, 0, fb - pb);
+        if (i == 1)
+          for (uint32_t j = 0; j < pb; ++j) f[j] = (uint8_t)j;
+      }
+    });
+  for (auto& x : th) x.join();
 }
 
 void free_client(client* c) {  // client.cpp:35-41
-  for (int i = 0; i < NUM_FILES; ++i) free(c->unencoded_files[i]);
+  big_free(c->ctx);  // the files' block
+  c->ctx = nullptr;
   free(c->unencoded_files);
   c->unencoded_files = nullptr;
 }
 
+// the nq the mode's queries will ask the engine for (engine_for's callers below)
+static int setup_nq() { return MODE == 1 ? NUM_RSS_KEYS : (MODE == 4 ? NUM_CD_KEYS : NUM_ROUNDS); }
+
+// A setup encodes on the GPU when the rows are still initializeServer's zeros (the reference
+// XORs the encoding INTO the rows, client.cpp:66/88, so that is the whole result); the shard is
+// then resident and the first query answers from HBM.  Otherwise, and for servers this shim did
+// not initialise, the host encode below.
+static bool gpu_setup(server* s, const std::function<int(pir_engine_t*)>& encode) {
+  if (!s->ctx || getenv("PIR_SHIM_HOST_SETUP")) return false;
+  ShimState* st = static_cast<ShimState*>(s->ctx);
+  std::lock_guard<std::mutex> lk(st->mu);
+  if (!st->rows_zero) {  // rows already hold data: the host XOR-encode keeps that data
+    std::unique_lock<std::shared_mutex> excl(st->life);
+    sync_rows_down(s, st);
+    return false;
+  }
+  pir_engine_t* e = engine_for(s, st, setup_nq(), /*upload=*/false, /*must=*/false);
+  if (!e) {  // no usable GPU here: the reference's host encode (queries will refuse loudly)
+    st->dirty = true;
+    return false;
+  }
+  if (encode(e) != PIR_OK) die("encode on the GPU");
+  st->dirty = false;
+  st->host_stale = true;
+  st->rows_zero = false;
+  return true;
+}
+
 // client.cpp:70-97: row i of party q = XOR_j gf_pow(q, j) * file[encDBsize*j + i]
 void encode_across_files_server(client* c, server* s) {
+  if (gpu_setup(s, [&](pir_engine_t* e) {
+        return pir_engine_encode_across_rows(e, c->unencoded_files, (uint64_t)NUM_FILES, K);
+      }))
+    return;
   const long encdb = (NUM_FILES + K - 1) / K;
   const int efs = ENCODED_FILE_SIZE_BYTES;
   std::vector<uint8_t> coef(K);
@@ -979,7 +1157,7 @@ void encode_across_files_server(client* c, server* s) {
       for (int b = 0; b < efs; ++b) row[b] ^= gf_mul_h(f[b], coef[j]);
     }
   }
-  if (s->ctx) static_cast<ShimState*>(s->ctx)->dirty = true;
+  shard_written_on_host(s);
 }
 
 // client.cpp:43-56, 99-103: row i of party q = XOR_{j<K} gf_pow(q, j) * part j of file i, where
@@ -987,6 +1165,11 @@ void encode_across_files_server(client* c, server* s) {
 // gen_encode_matrix, coding.cpp:64-70).  One 256-entry product table per coefficient.
 void encode_within_files_server(client* c, server* s) {
   if (IS_HERMITE) out_of_scope("encode_within_files_server (Hermite rows)", "Shamir");
+  if (gpu_setup(s, [&](pir_engine_t* e) {
+        return pir_engine_encode_within_rows(e, c->unencoded_files, (uint64_t)NUM_FILES,
+                                             FILE_SIZE_BYTES, K, s->partyIndex);
+      }))
+    return;
   const int efs = ENCODED_FILE_SIZE_BYTES;
   std::vector<uint8_t> tab((size_t)K * 256);
   for (int j = 0; j < K; ++j) {
@@ -1004,7 +1187,7 @@ void encode_within_files_server(client* c, server* s) {
       }
     }
   }
-  if (s->ctx) static_cast<ShimState*>(s->ctx)->dirty = true;
+  shard_written_on_host(s);
 }
 
 // ---- client-side names of package c (src/client/*.go, src/benchmark/benchmark.go) ----------

@@ -355,11 +355,11 @@ class Engine:
 
     def trace_query(self, d_key, num_keys=1):
         """One single-launch answer of a queue of num_keys keys (at d_key, key_len apart) with
-        per-workgroup phase stamps (diagnostics): an array [workgroups, 192] of microseconds
+        per-workgroup phase stamps (diagnostics): an array [workgroups, 256] of microseconds
         since the earliest workgroup start (layout: pir_engine_trace_query in
-        include/pir_engine.h; 0 = stamp not reached; columns 56-57 and 128-159 are raw shader-clock
-        ticks, divided by 100 like the rest)."""
-        out = np.zeros((4096, 192), np.uint64)
+        include/pir_engine.h; 0 = stamp not reached; columns 56-57, 128-159 and 192-255 are raw
+        shader-clock ticks or counts, divided by 100 like the rest)."""
+        out = np.zeros((4096, 256), np.uint64)
         n = self._lib.pir_engine_trace_query(self._h, d_key, num_keys,
                                              out.ctypes.data_as(ctypes.c_void_p), 4096)
         check(min(n, 0), "trace_query")
@@ -373,6 +373,16 @@ class Engine:
     def detach_comm(self):
         """Drop the communicator (aborted): this engine answers its partition alone again."""
         check(self._lib.pir_comm_detach(self._h), "pir_comm_detach")
+
+    def comm_info(self):
+        """RCCL's own view of this engine's communicator (ncclCommCount, ncclCommUserRank,
+        ncclCommCuDevice; -1 when none is attached) and the engine device's PCI bus id."""
+        ci = _lib.PirCommInfo()
+        check(self._lib.pir_comm_info(self._h, ctypes.byref(ci)), "pir_comm_info")
+        return {"attached": bool(ci.attached), "rccl_count": ci.count,
+                "rccl_user_rank": ci.user_rank, "rccl_device": ci.device,
+                "engine_device": ci.engine_device,
+                "pci_bus_id": ci.pci_bus_id.decode(errors="replace")}
 
 
 def mp_num_keys(p, t):

@@ -56,6 +56,9 @@ class Server:
                                    self.file_size)
 
     def read_row(self, i):
+        """indexList[i] (after a GPU setup the rows are first synced from the device shard:
+        pirServerSyncRows, a no-op once they are current)."""
+        self._lib.pirServerSyncRows(ctypes.byref(self.s))
         return np.ctypeslib.as_array(self.s.indexList[i], (self.file_size,)).copy()
 
     def runOptimizedDPFTreeQuery(self, key, numQueries):

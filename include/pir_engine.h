@@ -78,8 +78,14 @@ int pir_engine_set_party_index(pir_engine_t *e, int party_index);
 /* rows [row0, row0+nrows) from a host buffer with src_pitch bytes between rows */
 int pir_engine_set_shard(pir_engine_t *e, const uint8_t *host, uint64_t row0, uint64_t nrows,
                          uint64_t src_pitch);
-/* rows [row0, row0+nrows) from an array of row pointers (server.indexList) */
+/* rows [row0, row0+nrows) from an array of row pointers (server.indexList): host threads
+ * ($PIR_GATHER_THREADS, default min(8, cores)) gather ~64 MiB chunks into two pinned buffers,
+ * chunk c + 1 while the DMA of chunk c runs */
 int pir_engine_set_shard_rows(pir_engine_t *e, const uint8_t *const *rows, uint64_t row0,
+                              uint64_t nrows);
+/* the reverse: rows [row0, row0+nrows) of the device shard into row pointers (record_bytes
+ * each), DMA into two pinned buffers, host threads scattering one while the other fills */
+int pir_engine_get_shard_rows(pir_engine_t *e, uint8_t *const *rows, uint64_t row0,
                               uint64_t nrows);
 /* synthetic shard generated on the device (bench): byte b of GLOBAL row i is a function of
  * (seed, i, b), so every partition of a logical shard agrees with the whole */
@@ -91,6 +97,16 @@ int pir_engine_fill_shard_random(pir_engine_t *e, uint64_t seed);
  * reference's synthetic database (client.cpp:16-33). */
 int pir_engine_encode_across_dev(pir_engine_t *e, const uint8_t *d_files, uint64_t file_pitch,
                                  uint64_t num_files, int k);
+/* pir_engine_encode_across_dev from the client's HOST file rows (client.unencoded_files:
+ * num_files row pointers, record_bytes read from each): the server setup of server.go:299-331
+ * with the encode on the GPU.  Per ~64 MiB chunk of this engine's rows, host threads gather the
+ * k source files of each row into pinned staging (chunk c + 1 while chunk c's DMA and encode
+ * kernel run); the shard is left resident in HBM. */
+int pir_engine_encode_across_rows(pir_engine_t *e, const uint8_t *const *files,
+                                  uint64_t num_files, int k);
+/* the same for pir_engine_encode_within_dev: num_files host rows of file_bytes each */
+int pir_engine_encode_within_rows(pir_engine_t *e, const uint8_t *const *files,
+                                  uint64_t num_files, uint32_t file_bytes, int k, int party);
 /* the Hollanti-mode shard (MODE 3: encoded within files), computed on the GPU (client.cpp:43-56,
  * 99-103; replaces the host encode_within_files_server of the server setup): row r of this
  * engine's rows = XOR_{j<k} gf_pow(party, j) * part j of file r, part j = bytes
@@ -218,14 +234,15 @@ int pir_engine_last_timings(pir_engine_t *e, pir_kernel_time *out, int max);
  * all rows), reduce.  d_key: device pointer to one raw key. */
 int pir_engine_profile_phases(pir_engine_t *e, const uint8_t *d_key, int iters, float *out_ms);
 /* diagnostics: one single-launch answer (k_query) of a queue of num_keys keys with
- * per-workgroup phase stamps.  out holds max_wgs x 128 uint64 wall-clock ticks (100 MHz)
+ * per-workgroup phase stamps.  out holds max_wgs x 256 uint64 wall-clock ticks (100 MHz)
  * relative to the earliest start (0 = not reached): [0..6] start, key parsed, first tile root,
  * tile 0 shares ready, last tile of query 0 ready, query 0 scanned, query 0 slab written;
  * [8+d] descent level d of the first tile root (d < 32); [40+l] expansion level l of tile 0
  * (l < 16); [56], [57] shader clock (s_memtime) at start and at the first tile root; [64+g]
  * queue tile g ready, [96+g] queue tile g consumed by scan wave 0, [128+g] shader clock at
  * [64+g] (g < 32); [160+l] expansion level l of queue tile 1 (built by the tree waves beside
- * the scan), [176] its root ready.  Returns the number
+ * the scan), [176] its root ready; [192+8w+k] (diagnostic builds with -DPIR_FOLD_STAMPS=1
+ * only) shader cycles of fold phase k of four-Russians scan wave w.  Returns the number
  * of workgroups (>= 0), or an error code; PIR_EINVAL when the shape does not use k_query. */
 int pir_engine_trace_query(pir_engine_t *e, const uint8_t *d_key, int num_keys, uint64_t *out,
                            int max_wgs);
@@ -245,6 +262,19 @@ int pir_comm_attach(pir_engine_t *e, const uint8_t id[PIR_COMM_ID_BYTES], int nr
  * with no answer in flight: it waits for the engine's own stream only, and an exchange enqueued
  * on a caller's stream would be cut off by the abort. */
 int pir_comm_detach(pir_engine_t *e);
+/* what RCCL and HIP report for this engine (a multi-GPU run's self-check): attached = 1 when a
+ * communicator is attached; count, user_rank and device = ncclCommCount, ncclCommUserRank and
+ * ncclCommCuDevice of that communicator (-1 when none); engine_device = the engine's HIP device;
+ * pci_bus_id = hipDeviceGetPCIBusId of it (so N ranks can be checked to sit on N distinct GPUs). */
+typedef struct pir_comm_info {
+  int attached;
+  int count;
+  int user_rank;
+  int device;
+  int engine_device;
+  char pci_bus_id[64];
+} pir_comm_info_t;
+int pir_comm_info(pir_engine_t *e, pir_comm_info_t *out);
 /* the combine step after the all-gather, on its own: d_gathered = nranks blocks of
  * bytes_per_rank (rank r's partial answers at r * bytes_per_rank: ncclAllGather's output
  * layout); d_result[i] = XOR over r of d_gathered[r * bytes_per_rank + i] (the XOR assembly of

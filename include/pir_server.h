@@ -36,6 +36,20 @@
  *     (params.cpp:12, :372): the reference keeps the M = 2 of a K = 2, B = 1 CD setup
  *     (params.cpp:440) and a cleared isRss (:520-599) for all later calls;
  *   - no Woodruff MAPPING_INDEX tables (params.cpp:621-640; out of scope, and overflowing).
+ *
+ * Setup (src/server/server.go:299-331: setSystemParams, initialize_client, initializeServer,
+ * encode_*_files_server): the encode runs on the GPU from the client's host files and leaves the
+ * shard resident in HBM, so the first query after a setup answers from device memory.  indexList
+ * is then materialised lazily: the shim itself syncs it back before anything reads or writes the
+ * host rows (an engine re-creation, pirServerSetRows, a second encode); a C caller that reads or
+ * writes indexList directly after a setup calls pirServerSyncRows first ($PIR_SHIM_HOST_SETUP=1:
+ * the reference's host encode into indexList, uploaded lazily on the first query).
+ *
+ * Cost model of runOptimizedDPFTreeQueryThread: the first of a query's T calls (same key, same T)
+ * answers all T slices in ONE shard pass (pir_engine_answer_slices), the others copy their slice
+ * out of it; a caller that issues slices of a query one at a time, or spreads them over servers,
+ * pays a full pass per call.  At most 8 queries' slice groups (and 256 MiB of their parts) are
+ * kept; the oldest is dropped first.
  */
 #ifndef PIR_SERVER_H
 #define PIR_SERVER_H
@@ -46,7 +60,7 @@ extern "C" {
 #endif
 
 typedef struct {
-    void *ctx;          /* pir_engine_t* (created lazily on the first query) */
+    void *ctx;          /* the shim's engine state (engine created at setup or first query) */
     void **ctxThreads;  /* unused, kept for field-name compatibility        */
     int partyIndex;
     uint8_t **indexList;
@@ -224,8 +238,12 @@ void pirRunTreeQueryThreads(server *s, uint8_t *key, int numThreads, uint8_t **r
 /* Engine device used by servers created after this call (default: $PIR_DEVICE or 0). */
 void pirSetDevice(int device);
 /* indexList rows were written by something other than encode_across_files_server: the next
- * query re-uploads the shard to HBM (encode_across_files_server does this implicitly). */
+ * query re-uploads the shard to HBM (encode_across_files_server does this implicitly).  After a
+ * GPU setup, call pirServerSyncRows BEFORE writing the rows directly. */
 void pirServerShardChanged(server *s);
+/* After a setup that encoded on the GPU: copy the device shard into indexList (no-op if the
+ * host rows are current).  For C callers that read or write indexList directly. */
+void pirServerSyncRows(server *s);
 /* Harness helper (no reference counterpart): copy `nrows` packed rows of `rowBytes` bytes
  * (rowBytes <= the server's fileSizeBytes) into indexList[row0 ..] and mark the shard changed
  * -- what a test or benchmark would otherwise do row by row through indexList. */

@@ -148,3 +148,18 @@ def test_errors_are_loud_without_a_gpu():
     from erasurecodedpir_amd import Engine, PirError
     with pytest.raises(PirError):
         Engine(2, 1, 10, 16, 1)
+
+
+def test_cd_key_counts_reset_per_setup():
+    """setSystemParams starts from a fresh process's covering-design counts (params.cpp:368-369,
+    NUM_CD_KEYS = 2, NUM_CD_KEYS_NEEDED = 4): a CD842 setup (K = 2, B = 1: p = 8, M = 2 ->
+    3 / 6, params.cpp:519-599) followed by a mode-4 setup that matches no covering design
+    (T = 2, K = 1, R = 1, B = 0: p = 8, M = 4) leaves the CD532 defaults, not CD842's counts."""
+    from erasurecodedpir_amd import _lib as L
+    from erasurecodedpir_amd import server
+    server.setSystemParams(10, 64, 2, 2, 0, 1, 1, 0, 4)
+    assert (L.global_int("NUM_PARTIES"), L.global_int("NUM_CD_KEYS"),
+            L.global_int("NUM_CD_KEYS_NEEDED")) == (8, 3, 6)
+    server.setSystemParams(10, 64, 2, 1, 1, 0, 1, 0, 4)
+    assert (L.global_int("NUM_PARTIES"), L.global_int("NUM_CD_KEYS"),
+            L.global_int("NUM_CD_KEYS_NEEDED")) == (8, 2, 4)

@@ -152,6 +152,64 @@ __device__ __forceinline__ void m4r_fold4p<{vec}, {na}>(uint32_t (&Z)[{na}][8][{
 """
 
 
+def fold_sgpr(vec, na):
+    """m4r_fold4p with round a's packed plane indices already in an SGPR (p[a], bits [4b, 4b + 4)
+    = plane (a, b)'s index): the k_query scan waves build the packed words of all 64 groups of a
+    tile at once, one group per lane (m4r_tile_index), and read group G's with v_readlane before
+    the statement -- no readlane, DPP pack or wait state inside it."""
+    base = 128 - 16 * vec
+    lines = ["s_mov_b32 %[m0s], m0"]
+    n = 8 * na
+    ahead = 3
+    def reg(k):
+        return f"s{k % (ahead + 1)}"
+    def bfe(k):
+        return f"s_bfe_u32 %[{reg(k)}], %[p{k // 8}], {hex((4 << 16) | (4 * (k % 8)))}"
+    comb = []
+    for v in range(vec):
+        comb += combos(base + 16 * v, [f"%[x{i}{v}]" for i in range(4)])
+    lines += comb[:8] + [bfe(k) for k in range(min(ahead, n))] + comb[8:]
+    lines.append("s_set_gpr_idx_on %[s0], gpr_idx(SRC0)")
+    for k in range(n):
+        if k + ahead < n:
+            lines.append(bfe(k + ahead))
+        lines.append("@PACK_WAIT" if k + ahead < n else "@NOP_IDX")
+        a, b = divmod(k, 8)
+        for v in range(vec):
+            z = (a * vec + v) * 8 + b
+            lines.append(f"v_xor_b32 %{z}, v{base + 16 * v}, %{z}")
+        if k + 1 < n:
+            lines.append(f"s_set_gpr_idx_idx %[{reg(k + 1)}]")
+    lines.append("s_set_gpr_idx_off")
+    lines.append("s_mov_b32 m0, %[m0s]")
+    def emit(ln):
+        if ln == "@NOP_IDX":
+            return "      PIR_M4R_NOP_IDX"
+        if ln == "@PACK_WAIT":
+            return "      PIR_M4R_PACK_NOP"
+        return f'      "{ln}\\n\\t"'
+    body = "\n".join(emit(ln) for ln in lines)
+    zops = ", ".join(f'"+v"(Z[{a}][{b}][{v}])' for a in range(na) for v in range(vec)
+                     for b in range(8))
+    sops = ", ".join([f'[s{i}] "=&s"(s{i})' for i in range(ahead + 1)] + ['[m0s] "=&s"(m0s)'])
+    xins = ", ".join(f'[x{i}{v}] "v"(x{i}[{v}])' for i in range(4) for v in range(vec))
+    pins = ", ".join(f'[p{a}] "s"(p[{a}])' for a in range(na))
+    clob = ", ".join([f'"v{r}"' for r in range(base, 128)] + ['"scc"'])
+    return f"""template <>
+__device__ __forceinline__ void m4r_fold4s<{vec}, {na}>(uint32_t (&Z)[{na}][8][{vec}], const uint32_t* x0,
+                                            const uint32_t* x1, const uint32_t* x2,
+                                            const uint32_t* x3, const uint32_t* p) {{
+  uint32_t {", ".join(f"s{i}" for i in range(ahead + 1))}, m0s;
+  asm volatile(
+{body}
+      : {zops},
+        {sops}
+      : {xins}, {pins}
+      : {clob});
+}}
+"""
+
+
 def main():
     out = ['// GENERATED by tools/gen_m4r.py -- do not edit.  Four-Russians plane folds (see there).',
            '#pragma once', '#include <hip/hip_runtime.h>', '#include <stdint.h>', '',
@@ -182,10 +240,17 @@ def main():
            'template <int VEC, int NA>',
            '__device__ __forceinline__ void m4r_fold4p(uint32_t (&Z)[NA][8][VEC], const uint32_t* x0,',
            '                                           const uint32_t* x1, const uint32_t* x2,',
-           '                                           const uint32_t* x3, uint32_t vp);', '']
+           '                                           const uint32_t* x3, uint32_t vp);', '',
+           '// The same fold from packed indices already in SGPRs: p[a] = round a\'s 8 plane indices.',
+           'template <int VEC, int NA>',
+           '__device__ __forceinline__ void m4r_fold4s(uint32_t (&Z)[NA][8][VEC], const uint32_t* x0,',
+           '                                           const uint32_t* x1, const uint32_t* x2,',
+           '                                           const uint32_t* x3, const uint32_t* p);', '']
     for vec, na in VARIANTS:
         out.append(fold(vec, na))
         out.append(fold_packed(vec, na))
+        if vec == 2 and na >= 3:  # k_query's four-Russians scan waves (3-5 rounds)
+            out.append(fold_sgpr(vec, na))
     out.append('}  // namespace pir')
     print("\n".join(out))
 

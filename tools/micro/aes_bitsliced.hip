@@ -137,7 +137,6 @@ static int timed(const char* name, F launch, double nodes) {
 int main() {
   int cus;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  pir::upload_te0(0);
   uint32_t* out;
   CK(hipMalloc(&out, (size_t)cus * 4096 * 4 * 8));
   // correctness against the T-table AES: 64 quads x 32 nodes

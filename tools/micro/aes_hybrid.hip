@@ -95,7 +95,6 @@ static int run(int cus, unsigned long long* d_cnt, uint32_t* out) {
 int main() {
   int cus;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  pir::upload_te0(0);
   unsigned long long* d_cnt;
   uint32_t* out;
   CK(hipMalloc(&d_cnt, 2 * sizeof(unsigned long long)));

@@ -81,7 +81,6 @@ static void run(const char* name, void (*launch)()) {
 }
 
 int main() {
-  upload_te0(nullptr);
   (void)hipMalloc(&g_o, 256 * 1024 * 4);
   (void)hipMalloc(&g_c, 8);
   run("col", [] { hipLaunchKernelGGL(k_col, dim3(1), dim3(64), 0, 0, kIters, g_o, g_c); });

@@ -57,7 +57,6 @@ int main() {
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   uint32_t* out;
   CK(hipMalloc(&out, (size_t)cus * 1024 * 4));
-  pir::upload_te0(0);
   run<3>(cus, out, 2000);
   run<1>(cus, out, 4000);
   run<3>(cus, out, 2000);
