@@ -491,6 +491,33 @@ def _pmc_traffic(config, world, queries_per_launch):
         return None, None
 
 
+def _c3b_ceilings():
+    """configs[2]'s bound, from the committed per-kernel counters (profiles/pmc_c3b.json,
+    tools/pmc_kernels.py; quoted only when they were taken on the loaded library): the leaf stage
+    (k_subtree, ~77 % of the step) is LDS-lookup-bound -- its conflict-free LDS-array cycles over
+    its duration -- and k_scan_t is LDS-bound through bank conflicts."""
+    path = os.path.join(ROOT, "profiles", "pmc_c3b.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    cur = _pmc_current(d)
+    ks = d.get("kernels", {})
+    leaf, scan = ks.get("k_subtree<false", {}), ks.get("k_scan_t", {})
+    if not leaf.get("ceilings"):
+        return None
+    lc, sc = leaf["ceilings"], scan.get("ceilings", {})
+    return {"bound": "lds", "unit": "fraction of the LDS-array ceiling (32 lookups/clk/CU)",
+            "kernel": "k_subtree leaf stage (8 keys x 2^24 leaves per launch)",
+            "frac": lc.get("lds_frac_of_ceiling"),
+            "lds_lookups_per_leaf": leaf.get("derived", {}).get("lds_lane_ops_per_leaf"),
+            "valu_frac": lc.get("valu_frac_of_ceiling"),
+            "scan_kernel": "k_scan_t (transposed four Russians, 64 planes)",
+            "scan_lds_busy_with_conflicts": sc.get("lds_busy_share_with_conflicts"),
+            "scan_lds_conflict_share": scan.get("derived", {}).get("lds_bank_conflict_share_of_lds_cycles"),
+            "source": "profiles/pmc_c3b.json" + ("" if cur else " (stale: another libpir_engine.so build)")}
+
+
 def r5(x):
     return round(float(x), 5)
 
@@ -692,9 +719,9 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_extras:
         # the drop-in's setup -> first answer (north_star shape; configs[4]'s per-server shape)
-        out["setup_c24"] = setup_leg(ctx, pir, 24, 1024, 1, 1)
+        out["setup_c24"] = setup_leg(ctx, pir, 24, 1024, 1, 0)  # k = 1, r = 0: p = 2
         out["setup_c5"] = setup_leg(ctx, pir, 26, 1024, 5, 2, party=3)
-        out["configs1_c2"] = extra_leg(ctx, pir, "c2", W, K, rng)
+        out["configs1_c2"] = batch1_first(extra_leg(ctx, pir, "c2", W, K, rng))
         if config != "c4":
             out["c4_single_engine"] = extra_leg(ctx, pir, "c4", min(W, 2), min(K, 16), rng,
                                                 single=False)
@@ -706,6 +733,7 @@ def main():
                                                  "ms_per_step", "ms_per_key", "keys_per_s",
                                                  "shard_passes_per_step", "parity")}
         out["configs2_c3b"]["workload"] = b["config"]["workload"]
+        out["configs2_c3b"]["roofline"] = _c3b_ceilings()
     if cpu_path and args.no_cpu:
         os.unlink(cpu_path)
     elif cpu_path:
@@ -716,6 +744,8 @@ def main():
             out["parity"]["gpu_equals_cpu_reference"] = out["cpu_baseline"]["bit_exact_vs_gpu"]
         finally:
             os.unlink(cpu_path)
+        if not args.no_extras and os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libref.so")):
+            out["cpu_baselines"] = per_config_cpu(ctx, pir, rng, out["cpu_baseline"])
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -826,6 +856,80 @@ def extra_leg(ctx, pir, config, W, K, rng, single=True):
         res["queue_equals_one_at_a_time"] = bool(np.array_equal(m["answers"], m["singles"]))
     else:
         res["queue_equals_one_at_a_time"] = bool(q1)
+    return res
+
+
+def cpu_sample(ctx, pir, rng, n, efs, p, nq, full_n, what):
+    """The reference (oracle/_ref/libref.so) answering one query of a BASELINE config's shape on
+    one host core, at 2^n rows (full_n: the config's own size), bit-exact against the GPU's
+    answer of the same key over the same shard.  Its GiB/s is size-independent to first order
+    (the reference's tree and scan are both linear in the rows), so a sample at fewer rows is
+    reported as that config's rate, labelled."""
+    keyset, _ = make_keys(pir, n, p, nq, 1, rng, ctx.local)
+    key = keyset[0][1][0]
+    eng = pir.Engine(p, 1, n, efs, nq, device=ctx.local)
+    try:
+        eng.fill_shard_random(SHARD_SEED)
+        want = eng.answer(key)
+        path = shard_file_path((1 << n) * efs)
+        dump_shard(eng, path)
+    finally:
+        eng.close()
+    try:
+        L = _ref_lib()
+        shard = np.memmap(path, np.uint8, mode="r")
+        keyb = np.frombuffer(bytes(key), np.uint8).copy()
+        res = np.zeros(nq * efs, np.uint8)
+        P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        h = L.ref_server_view(p, 1, n, efs, nq, P(shard))
+        t = L.ref_server_time(h, P(keyb), P(res), 1)
+        L.ref_server_view_free(h)
+        del shard
+    finally:
+        os.unlink(path)
+    gib = (1 << n) * efs / GIB
+    return {"workload": what, "value": round(gib / t, 4), "unit": "GiB/s", "cores": 1,
+            "kind": "reference", "s_per_query": round(t, 4),
+            "s_per_query_at_full_size": round(t * (1 << (full_n - n)), 2),
+            "sample": (f"1 query at 2^{n} x {efs} B, p={p}, NUM_ROUNDS={nq} on 1 host core"
+                       + ("" if n == full_n else f" (the config has 2^{full_n} rows: the full-size "
+                                                 f"time is scaled by 2^{full_n - n})")),
+            "bit_exact_vs_gpu": bool(np.array_equal(res.reshape(nq, efs), want))}
+
+
+def per_config_cpu(ctx, pir, rng, main_leg):
+    """BASELINE.md section 3's per-config CPU figures: the reference src/c path
+    (runOptimizedDPFTreeQuery, server.cpp:96-134) on one host core for every config shape."""
+    out = {
+        "configs1_c2": cpu_sample(ctx, pir, rng, 20, 1024, 2, 1, 20,
+                                  "configs[1]: 2^20 x 1 KiB, p=2, one query (full size)"),
+        "configs2_c3_per_key": cpu_sample(ctx, pir, rng, 20, 256, 2, 1, 24,
+                                          "configs[2]: 2^24 x 256 B, p=2 -- per key (the "
+                                          "reference has no batched answer: 128 keys = 128 queries)"),
+        "configs4_c5": cpu_sample(ctx, pir, rng, 18, 1024, 8, 5, 24,
+                                  "configs[4] per server: 2^24 x 1 KiB, p=8, NUM_ROUNDS=5"),
+    }
+    t24 = main_leg.get("s_per_query")
+    if t24:
+        out["configs3_c4"] = {
+            "workload": "configs[3]: one logical 2^27 x 1 KiB server (8 x 2^24 partitions)",
+            "value": round(128.0 / (8 * t24), 4), "unit": "GiB/s", "cores": 1, "kind": "reference",
+            "s_per_query_at_full_size": round(8 * t24, 2),
+            "sample": "derived: 8 x the 2^24 x 1 KiB query timed in cpu_baseline (the reference "
+                      "cannot evaluate a depth-27 tree: int overflow, dpf_tree.cpp:484-485)"}
+    return out
+
+
+def batch1_first(res):
+    """configs[1] is defined at batch = 1 (BASELINE.json configs[1]): its value and ms_per_query
+    are the one-launch-per-query figures; the queue's stay beside them as `queue`."""
+    sq = res.pop("single_query")
+    res["queue"] = {"ms_per_query": res.pop("ms_per_query"), "value": res.pop("value"),
+                    "unit": "GiB/s", "k_query_ms_per_launch": res.pop("k_query_ms_per_launch"),
+                    "roofline_frac": res.pop("roofline_frac"),
+                    "note": "the same K queries answered as ONE queued launch"}
+    res.update(ms_per_query=sq["ms_per_query"], value=sq["value"], unit="GiB/s",
+               value_kind="batch = 1: one launch per query (answer_dev), K queries back to back")
     return res
 
 

@@ -3,6 +3,13 @@
 
     python tools/pmc_kernels.py CFG OUT.json KERNEL=UNITS:UNITNAME ...
 
+Also written (round 5): the library the passes ran (lib_sha256, from tools/gpu_pmc.sh's
+gpurun_out/pmc_<CFG>_lib_sha256.txt), each kernel's average duration in the kernel-trace pass
+(gpurun_out/prof_<CFG>/run_kernel_stats.csv) and its LDS and VALU floors at the clock the counters
+imply: conflict-free LDS-array cycles per CU ((SQ_LDS_IDX_ACTIVE - SQ_LDS_BANK_CONFLICT) / 256)
+and VALU issue cycles per SIMD (SQ_INSTS_VALU / 1024 x 2: a wave64 op holds a SIMD-32 for 2
+cycles), each over the kernel's duration -- the kernel's fraction of its LDS / VALU ceiling.
+
 For each named kernel (a substring of its demangled name) every counter of every pass
 gpurun_out/pmc_<CFG>_*/run_counter_collection.csv is averaged over that kernel's launches, and
 derived per unit of work: VALU / SALU / LDS lane-ops per unit (SQ_INSTS_* x 64 / units per launch),
@@ -57,8 +64,38 @@ def main():
             per["valu_insts_per_simd_per_cycle"] = round(avg["SQ_INSTS_VALU"] / (256 * 4) / gui, 4)
         d["derived"] = per
         res["kernels"][name] = d
+    shaf = os.path.join(ROOT, "gpurun_out", f"pmc_{cfg}_lib_sha256.txt")
+    if os.path.exists(shaf):
+        res["lib_sha256"] = open(shaf).read().split()[0]
+    stats = os.path.join(ROOT, "gpurun_out", f"prof_{cfg}", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        rows = list(csv.DictReader(open(stats)))
+        for name, _, _ in specs:
+            hit = [r for r in rows if name in r["Name"]]
+            d = res["kernels"][name]
+            if not hit:
+                continue
+            avg_ns = float(hit[0]["AverageNs"])
+            a = d["counters_avg_per_launch"]
+            d["kernel_avg_ns_trace"] = avg_ns
+            if "GRBM_GUI_ACTIVE" in a:
+                # the counter passes' own clock: their cycles over the traced duration
+                gui = a["GRBM_GUI_ACTIVE"] / 8
+                ghz = gui / avg_ns
+                c = {"shader_clock_GHz_implied": round(ghz, 3)}
+                if "SQ_LDS_IDX_ACTIVE" in a:
+                    lds = (a["SQ_LDS_IDX_ACTIVE"] - a.get("SQ_LDS_BANK_CONFLICT", 0.0)) / 256
+                    c["lds_floor_ns"] = round(lds / ghz, 1)
+                    c["lds_frac_of_ceiling"] = round(lds / gui, 4)
+                    c["lds_busy_share_with_conflicts"] = round(a["SQ_LDS_IDX_ACTIVE"] / 256 / gui, 4)
+                if "SQ_INSTS_VALU" in a:
+                    valu = a["SQ_INSTS_VALU"] / 1024 * 2
+                    c["valu_floor_ns"] = round(valu / ghz, 1)
+                    c["valu_frac_of_ceiling"] = round(valu / gui, 4)
+                d["ceilings"] = c
     json.dump(res, open(out, "w"), indent=1)
-    print(json.dumps({k: v["derived"] for k, v in res["kernels"].items()}, indent=1))
+    print(json.dumps({k: {**v["derived"], **v.get("ceilings", {})} for k, v in res["kernels"].items()},
+                     indent=1))
 
 
 if __name__ == "__main__":
