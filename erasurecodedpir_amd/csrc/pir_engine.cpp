@@ -138,6 +138,13 @@ struct pir_engine {
   size_t qscratch_cap = 0;
   uint32_t* d_qcnt = nullptr;     // k_query fused reduce: per-query slab counters (kept zero)
   int qcnt_cap = 0;
+  // k_query's end-of-query work stealing for a lone whole answer (StealArgs, pir_kernels.h):
+  // per-workgroup chunk counters + publication flags + last-tile shares, zeroed once; steal_gen
+  // numbers the launches that use it ($PIR_QUERY_STEAL=0 turns it off)
+  uint32_t* d_steal = nullptr;
+  size_t steal_cap = 0;
+  uint32_t steal_gen = 0;
+  int steal = PIR_QUERY_STEAL ? 3 : 0;
   // k_query's in-kernel reduce (no k_reduce launch), $PIR_FUSED_REDUCE: 0 = off (k_reduce);
   // 1 = the last workgroup XORs the slabs (measured slower for a lone 2^20 x 1 KiB query: kernel
   // 0.250 vs 0.218 ms, one workgroup's 256 KiB of cross-XCD sc1 loads outlast a k_reduce
@@ -303,6 +310,37 @@ int ensure_qcnt(pir_engine* e, int nk, hipStream_t s) {
   return PIR_OK;
 }
 
+// the work-stealing arguments of a k_query launch (empty = static tiles): a lone query (nk == 1)
+// answered whole (nslices == 1: a stolen chunk is folded into the thief's region slab) with one
+// column group, on at most one workgroup per CU (every workgroup resident, so the bounded wait
+// for unpublished last tiles never outlasts a late one's dispatch)
+int steal_args(pir_engine* e, const pir::QueryPlan& qp, int nk, int nslices, hipStream_t s,
+               pir::StealArgs* out) {
+  *out = pir::StealArgs{};
+  if (!PIR_QUERY_STEAL || !e->steal || nk != 1 || nslices != 1 || qp.shape.nq > 2 || !qp.shape.uniform ||
+      qp.shape.grid.y != 1 || (int)qp.shape.grid.x > e->num_cus || qp.m4r)
+    return PIR_OK;
+  // a captured launch would replay one generation: flags left equal to it by the previous
+  // replay would read as published shares
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIP_TRY(hipStreamIsCapturing(s, &cap));
+  if (cap != hipStreamCaptureStatusNone) return PIR_OK;
+  const size_t bytes = pir::query_steal_bytes(qp);
+  if (bytes > e->steal_cap) {
+    if (e->d_steal) (void)hipFree(e->d_steal);
+    e->d_steal = nullptr;
+    e->steal_cap = 0;
+    HIP_TRY(hipMalloc(&e->d_steal, bytes));
+    HIP_TRY(hipMemsetAsync(e->d_steal, 0, bytes, s));  // no flag equals a generation (>= 1)
+    e->steal_cap = bytes;
+  }
+  if (++e->steal_gen == 0) e->steal_gen = 1;
+  out->buf = e->d_steal;
+  out->gen = e->steal_gen;
+  out->mode = (uint32_t)e->steal;
+  return PIR_OK;
+}
+
 // one launch: key parse, tree and scan of nk queued keys (key_len apart) in k_query; then the
 // slab reduce of all nk answers (d_out: nk x nq x efs)
 // nslices > 1 (a power of two <= 2^qp.lr, nk == 1): d_out gets the nslices partial answers
@@ -322,6 +360,8 @@ int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, 
   if (fred == 3 && qp.lr < 3) fred = 1;
   if (nslices > 1) fred = 0;
   if (!rc && fred) rc = ensure_qcnt(e, nk * (fred == 3 ? 8 : 1), s);
+  pir::StealArgs steal;
+  if (!rc) rc = steal_args(e, qp, nk, nslices, s, &steal);
   if (rc) return rc;
   if (fred >= 2)  // the workgroups (mode 2) or slab groups (mode 3) XOR into zeroed answers
     HIP_TRY(hipMemsetAsync(d_out, 0, (size_t)nk * c.num_rounds * c.record_bytes, s));
@@ -338,7 +378,8 @@ int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, 
   HIP_TRY(pir::launch_query(qp, d_raw, (uint32_t)e->key_len, nk, c.num_parties,
                             c.log_num_records, c.party_index - 1, log_parts_total, prefix,
                             e->d_shard + row0 * e->pitch, e->d_slabs, e->d_qscratch, s, nullptr,
-                            fred ? d_out : nullptr, e->d_qcnt, c.record_bytes, (uint32_t)fred));
+                            fred ? d_out : nullptr, e->d_qcnt, c.record_bytes, (uint32_t)fred,
+                            steal));
   if (ev) {
     HIP_TRY(hipEventRecord(ev[EV_SCAN_E], s));
     HIP_TRY(hipEventRecord(ev[EV_PRERED], s));
@@ -953,6 +994,9 @@ int pir_engine_create(const pir_engine_config* cfg, pir_engine_t** out) {
     e->allow_query = !(qy && qy[0] == '0');
     const char* fr = getenv("PIR_FUSED_REDUCE");
     if (fr) e->fused_reduce = std::max(0, std::min(3, atoi(fr)));
+    // $PIR_QUERY_STEAL: 0 = off; else the kernel's StealArgs::mode (default 3)
+    const char* st = getenv("PIR_QUERY_STEAL");
+    if (st) e->steal = std::max(0, std::min(3, atoi(st)));
     const char* bg = getenv("PIR_BATCH_G");
     if (bg) e->batch_group = atoi(bg);
     const char* bb = getenv("PIR_BATCH_SCAN_BPC");
@@ -995,7 +1039,7 @@ void pir_engine_destroy(pir_engine_t* e) {
                   (void*)e->nodes.t[1], (void*)e->d_c, (void*)e->d_slabs, (void*)e->d_part,
                   (void*)e->d_gather, (void*)e->d_result, (void*)e->d_cb, (void*)e->d_gtmp,
                   (void*)e->d_bpart, (void*)e->d_bgather, (void*)e->d_qscratch, (void*)e->d_coef_stage,
-                  (void*)e->d_qcnt, (void*)e->d_mpkey,
+                  (void*)e->d_qcnt, (void*)e->d_steal, (void*)e->d_mpkey,
                   (void*)e->bnodes.s[0],
                   (void*)e->bnodes.s[1], (void*)e->bnodes.t[0], (void*)e->bnodes.t[1]})
     if (p) (void)hipFree(p);
@@ -1410,6 +1454,10 @@ int pir_engine_reserve_queue(pir_engine_t* e, int num_keys) {
   int rc = ensure_slabs(e, (size_t)num_keys * pir::query_slab_bytes(qp));
   if (!rc) rc = ensure_buf(&e->d_qscratch, &e->qscratch_cap, pir::query_scratch_bytes(qp));
   if (!rc && e->fused_reduce) rc = ensure_qcnt(e, num_keys * 8, e->stream);
+  if (!rc && num_keys == 1) {  // the stealing buffer (the generation is not advanced here)
+    pir::StealArgs st;
+    rc = steal_args(e, qp, 1, 1, e->stream, &st);
+  }
   if (!rc && e->comm) {
     const size_t total = (size_t)num_keys * c.num_rounds * c.record_bytes;
     rc = ensure_buf(&e->d_bpart, &e->bpart_cap, total);
@@ -1774,6 +1822,8 @@ int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, int num_keys, 
   const pir::ScanShape& sh = qp.shape;
   int rc = ensure_slabs(e, (size_t)num_keys * pir::query_slab_bytes(qp));
   if (!rc) rc = ensure_buf(&e->d_qscratch, &e->qscratch_cap, pir::query_scratch_bytes(qp));
+  pir::StealArgs steal;
+  if (!rc) rc = steal_args(e, qp, num_keys, 1, e->stream, &steal);
   if (rc) return rc;
   const int nwg = (int)sh.grid.x;
   const size_t bytes = (size_t)nwg * pir::kQueryTraceSlots * sizeof(uint64_t);
@@ -1789,7 +1839,8 @@ int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, int num_keys, 
   if (err == hipSuccess)
     err = pir::launch_query(qp, d_key, (uint32_t)e->key_len, num_keys, c.num_parties, c.log_num_records,
                             c.party_index - 1, c.log_num_partitions, (uint64_t)c.partition_index,
-                            e->d_shard, e->d_slabs, e->d_qscratch, e->stream, d_tr);
+                            e->d_shard, e->d_slabs, e->d_qscratch, e->stream, d_tr, nullptr,
+                            nullptr, 0u, 0u, steal);
   if (err == hipSuccess) err = hipMemcpyAsync(h.data(), d_tr, bytes, hipMemcpyDeviceToHost, e->stream);
   if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
   (void)hipFree(d_tr);
@@ -1800,8 +1851,10 @@ int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, int num_keys, 
   for (int w = 0; w < n; ++w)
     for (int k = 0; k < pir::kQueryTraceSlots; ++k) {
       const uint64_t v = h[(size_t)w * pir::kQueryTraceSlots + k];
-      const bool clk = k == 56 || k == 57 || (k >= 128 && k < 160) || k >= 192;  // shader-clock ticks
-      out[(size_t)w * pir::kQueryTraceSlots + k] = clk ? v : (v ? v - t0 : 0);
+      // shader-clock ticks and counts as they are
+      const bool raw = k == 56 || k == 57 || k == 59 || k == 60 || k == 61 ||
+                       (k >= 128 && k < 160) || k >= 192;
+      out[(size_t)w * pir::kQueryTraceSlots + k] = raw ? v : (v ? v - t0 : 0);
     }
   return nwg;
 }

@@ -180,11 +180,30 @@ size_t query_scratch_bytes(const QueryPlan& qp);
 // = nk zeroed counters, left zero); 2 = every workgroup adds its partial with memory-side
 // atomics; 3 = the last workgroup of each of 8 slab groups adds the group's XOR (qcnt = 8 nk
 // counters).  Modes 2-3: answers the host zeroed before the launch, efs % 4 == 0.
+// End-of-query work stealing for a lone whole-shard answer (nk == 1, 1-2 rounds, one column
+// group): the last tile's shares go to global memory and its rows past the scan waves' static
+// prefix are handed out in chunks through a per-workgroup counter, to its own scan waves and then
+// to any workgroup whose own work is done.  buf: 2 u32 per workgroup (chunk counter, published
+// generation) then TILE * NRP bytes of shares per workgroup; zero-initialised once; gen: a new
+// nonzero value per launch (0: off).  Per-slice answers (runs of slabs) must not use it.
+// Compiled in only by the diagnostic build (make diag: -DPIR_QUERY_STEAL=1): measured no faster
+// on configs[1] -- the last tiles' scan is HBM-bound, not imbalanced (profiles/r05/steal_*.txt)
+// -- and its code costs the two-round k_query registers (spills 10 -> 69 VGPRs)
+#ifndef PIR_QUERY_STEAL
+#define PIR_QUERY_STEAL 0
+#endif
+struct StealArgs {
+  uint32_t* buf = nullptr;
+  uint32_t gen = 0;
+  uint32_t mode = 3;  // bit 0: the tree waves fold chunks; bit 1: they help neighbours
+};
+size_t query_steal_bytes(const QueryPlan& qp);
 hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stride, int nk,
                         int p, int n, int party0, int log_parts, uint64_t prefix,
                         const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
                         uint64_t* trace = nullptr, uint8_t* out = nullptr,
-                        uint32_t* qcnt = nullptr, uint32_t efs = 0, uint32_t red_mode = 0);
+                        uint32_t* qcnt = nullptr, uint32_t efs = 0, uint32_t red_mode = 0,
+                        StealArgs steal = StealArgs{});
 // k_query for a sqrt(N) DPF key (multiparty / covering design, pir_mp.h's MpLayout): the tree
 // waves build each tile's shares from the key's seeds, toggles and correction words (mp_tile)
 // while the scan waves stream the shard; then launch_reduce as for launch_query.  nk keys

@@ -1369,7 +1369,7 @@ __global__ __launch_bounds__(NT) void k_query(
     uint4* __restrict__ fr_s, uint32_t* __restrict__ fr_t, const uint8_t* __restrict__ shard,
     uint32_t pitch, uint32_t cpr, uint32_t gy, uint8_t* __restrict__ slabs,
     uint64_t* __restrict__ trace, uint8_t* __restrict__ out, uint32_t* __restrict__ qcnt,
-    uint32_t efs, uint32_t red_mode, MpLayout mpl) {
+    uint32_t efs, uint32_t red_mode, MpLayout mpl, StealArgs stl) {
   // MPK: the queue's keys are sqrt(N) DPF keys of layout mpl (key_stride bytes apart; multiparty
   // or covering design), and the tree waves build each tile's shares with mp_tile instead of a
   // DPF tree; the scan waves, slabs and reduce are the same
@@ -1424,12 +1424,136 @@ __global__ __launch_bounds__(NT) void k_query(
     fr_t += (size_t)b << (kQueryKin + ls);
   }
   const uint64_t region_rows = (uint64_t)TILE << lt;
+  // end-of-query work stealing (StealArgs, pir_kernels.h): a lone whole answer, 1-2 rounds,
+  // records of one wave row
+  constexpr bool kSteal = PIR_QUERY_STEAL && UNI && !MPK && NQ <= 2 && NWV - TW >= 8;
+  const bool steal_on = kSteal && stl.buf && stl.gen && nk == 1 && gy == 1;
   // first row (in this engine's rows) of tile i of this workgroup
   auto tile_row0 = [&](uint32_t i) __attribute__((always_inline)) -> uint64_t {
     return (uint64_t)blockIdx.x * region_rows + (uint64_t)i * TILE;
   };
   const size_t slab_words = (size_t)NQ * GW;
   const size_t slab_q_words = (size_t)gy * gridDim.x * slab_words;  // one query's slabs
+
+  // ================================ end-of-query work stealing ==============================
+  // The lone query's last tile (every workgroup's) is split: its first kStealPre rows go to the
+  // scan waves' static slots, the rest are chunks of kStealRows rows claimed one at a time
+  // with an agent-scope atomic add on the owning workgroup's counter (StealArgs).  A claimed
+  // chunk is folded by ONE wave into its own planes Zs (the chunk's rows x its shares): the
+  // scan waves claim only their own workgroup's chunks (shares in the LDS ring); the tree
+  // waves, idle once the last tile is built, claim their own and then, with `search`, those
+  // of any workgroup that has published its last tile (shares from global memory) -- so the
+  // workgroups that finish early fold the late ones' rows.  A wave leaves when no published
+  // tile has chunks left and every tile is published (or the bounded wait ran out: a
+  // workgroup not yet resident cannot publish; the late ones then fold their own chunks).
+  // Each fold lands in the folding workgroup's slab; the answer is the XOR of all slabs.
+  constexpr int kStealU = 8;                    // rows per batch (the scan waves' U)
+  constexpr uint32_t kStealPre = kStealU * (NWV - TW);  // rows of the static prefix (gy == 1)
+  constexpr uint32_t kStealRows = 32;
+  constexpr uint32_t kStealChunks = TILE > kStealPre ? (TILE - kStealPre) / kStealRows : 0u;
+  static_assert(!kSteal || (TILE - kStealPre) % kStealRows == 0, "whole chunks");
+  constexpr uint64_t kStealWaitTicks = 6000;   // 60 us of the 100 MHz wall clock
+  constexpr uint32_t kStealVictims = 16;       // neighbours a workgroup's tree waves help
+  constexpr uint32_t kStealSearchWaves = 2;    // tree waves that help them (all fold own chunks)
+  auto steal_chunks = [&](uint32_t (&Zs)[NQ][8][VEC], auto& xs, const uint8_t* own_ring,
+                          bool search) __attribute__((always_inline)) {
+    constexpr int SU = (int)(sizeof(xs) / sizeof(xs[0]));  // rows per batch
+    static_assert(kStealRows % SU == 0 && SU <= kStealU, "batches of a chunk");
+    const uint32_t G = gridDim.x, b32 = (uint32_t)b, C = kStealChunks;
+    constexpr uint32_t CW = TILE * NRP / 4;  // share dwords of one tile
+    const uint32_t xoff = lane < cpr ? lane * (uint32_t)CH : 0u;
+    const uint64_t give_up = wall_clock64() + kStealWaitTicks;
+    uint32_t v = b32, folded = 0;  // chunks folded: own in the low half, others' in the high
+    for (;;) {
+      uint32_t k = 0;
+      if (lane == 0)
+        k = __hip_atomic_fetch_add(stl.buf + 2 * v, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      k = (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
+      if (k >= C) {
+        if (!search) break;
+        // a neighbour with chunks left: workgroups b + 1 .. b + kStealVictims (mod G: every
+        // XCD under round-robin dispatch), lane d - 1 checks b + d's flag (== gen: published)
+        // and counter (< C: chunks left) -- two cache lines per probe, one probe per ~1 us
+        // while a neighbour is unpublished (polling every workgroup's flags flooded the fabric
+        // and slowed the late trees: profiles/r05/steal_trace_v1.txt)
+        const uint32_t NV = G - 1 < kStealVictims ? G - 1 : kStealVictims;
+        uint32_t nv = G;
+        for (;;) {
+          uint32_t cand = b32 + lane + 1;
+          if (cand >= G) cand -= G;
+          const bool live = lane < NV;
+          uint32_t fl = 0, nx = C;
+          if (live) {
+            fl = __hip_atomic_load(stl.buf + 2 * cand + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            nx = __hip_atomic_load(stl.buf + 2 * cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          const uint64_t am = __ballot(live && fl == stl.gen && nx < C);
+          if (am) {  // the stealing waves of a workgroup start at different neighbours
+            const uint64_t hi = am & (~0ull << ((wave * 5u) % NV));
+            nv = (uint32_t)__builtin_amdgcn_readlane((int)cand, (int)__builtin_ctzll(hi ? hi : am));
+            break;
+          }
+          if (!__ballot(live && fl != stl.gen) || wall_clock64() > give_up) break;
+          __builtin_amdgcn_s_sleep(32);  // a neighbour's last tile is not published yet
+        }
+        if (nv >= G) break;
+        // no acquire fence (an L2 invalidate at agent scope): the shares are read with
+        // agent-scope loads issued after the flag's value came back
+        v = nv;
+        continue;
+      }
+      const bool own = v == b32;
+      folded += own ? 1u : 0x10000u;
+      const uint32_t r0 = kStealPre + k * kStealRows;  // rows of workgroup v's last tile
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(shard + ((uint64_t)v * region_rows + (uint64_t)(ntiles - 1) * TILE) * pitch),
+          (short)0, (int)(TILE * pitch), kBufRsrcWord3);
+      const uint32_t* cgl = stl.buf + 2 * (uint64_t)G + (uint64_t)v * CW;
+#pragma unroll 1
+      for (uint32_t u0 = 0; u0 < kStealRows; u0 += SU) {
+#pragma unroll
+        for (int u = 0; u < SU; ++u) xs[u] = load_chunk_buf<VEC>(rs, xoff, (r0 + u0 + u) * pitch);
+        // lane u < SU reads row u's shares, v_readlane broadcasts them
+        const uint32_t rr = r0 + u0 + (lane < (uint32_t)SU ? lane : 0u);
+        uint32_t cw;
+        if (own) {
+          cw = load_coef<NRP>(own_ring, rr).x;
+        } else {
+          const uint32_t w = __hip_atomic_load(cgl + rr * NRP / 4, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+          cw = NRP == 1 ? (w >> (8 * (rr & 3u))) & 0xffu : (w >> (16 * (rr & 1u))) & 0xffffu;
+        }
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const uint32_t cu = (uint32_t)__builtin_amdgcn_readlane((int)cw, u);
+#pragma unroll
+          for (int a = 0; a < NQ; ++a) {
+            const uint32_t ca = (cu >> (8 * a)) & 0xffu;
+#pragma unroll
+            for (int kk = 0; kk < 8; ++kk)
+              if (ca & (1u << kk)) {
+#pragma unroll
+                for (int vv = 0; vv < VEC; ++vv) Zs[a][kk][vv] ^= xs[u].v[vv];
+              }
+          }
+        }
+      }
+    }
+    return folded;
+  };
+  // trace: chunk counts ([59] others' by the tree waves, [60] own by the tree waves, [61] own
+  // by the scan waves) and the tree waves' last stealing stamp ([58])
+  auto steal_trace = [&](uint32_t folded, bool tree) __attribute__((always_inline)) {
+    if (trace && lane == 0) {
+      if (tree) {
+        __hip_atomic_fetch_add(trace + 59, (uint64_t)(folded >> 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(trace + 60, (uint64_t)(folded & 0xffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(trace + 58, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        __hip_atomic_fetch_add(trace + 61, (uint64_t)(folded & 0xffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  };
 
   // ======================================= tree work =======================================
   // tree_tile(g, nt, team): the shares of queue tile g (query g / T, tile g % T) into ring slot
@@ -1777,6 +1901,26 @@ __global__ __launch_bounds__(NT) void k_query(
       }
     }
     sync();  // every share of tile g is in the ring
+    if constexpr (kSteal) {
+      if (steal_on && g + 1 == total) {
+        // the last tile's shares and the chunk counter reset as agent-scope (write-through)
+        // stores, each thread's complete (vmcnt 0) before the barrier, then the generation
+        // published: other workgroups may now claim chunks of this tile (the reset is also
+        // ordered before this workgroup's own claims by the ready signal below).  No release
+        // FENCE: at agent scope that is an L2 writeback, and 32 of them per XCD (every
+        // workgroup's last tile) stalled the XCD's L2 for ~100 us (profiles/r05/steal_trace_v2.txt)
+        constexpr uint32_t CW = TILE * NRP / 4;
+        uint32_t* hdr = stl.buf + 2 * b;
+        uint32_t* cg = stl.buf + 2 * (uint64_t)gridDim.x + b * CW;
+        const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ring);
+        for (int w = tt; w < (int)CW; w += nt)
+          __hip_atomic_store(cg + w, r32[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tt == 0) __hip_atomic_store(hdr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (also a compiler barrier)
+        sync();
+        if (tt == 0) __hip_atomic_store(hdr + 1, stl.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     if (wave == 0) lds_signal(&sm.ready);
     if (trace && tt == 0 && (g == 0 || g == ntiles - 1)) trace[g == 0 ? 3 : 4] = wall_clock64();
     if (trace && tt == 0 && g < 32) { trace[64 + g] = wall_clock64(); trace[128 + g] = clock64(); }
@@ -1792,6 +1936,33 @@ __global__ __launch_bounds__(NT) void k_query(
       // slot g % RING free: every scan wave has consumed tile g - RING (per-slot counts)
       if (g >= (uint32_t)RING) lds_wait_geq_idle(&sm.consumed[g % RING], (g / RING) * SW);
       tree_tile(g, TW * 64, TW);
+    }
+    if constexpr (kSteal) {
+      if (steal_on) {  // chunks of the last tiles, then the planes into red[] (ready += 1)
+        uint32_t Zt[NQ][8][VEC];
+#pragma unroll
+        for (int a = 0; a < NQ; ++a)
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+            for (int vv = 0; vv < VEC; ++vv) Zt[a][kk][vv] = 0;
+        Chunk<VEC> xt[NQ == 1 ? kStealU : kStealU / 2];  // (two rounds: 64 plane VGPRs)
+        if (stl.mode & 1u)
+          steal_trace(steal_chunks(Zt, xt, sm.ring[(total - 1) % RING],
+                                   (stl.mode & 2u) && wave < kStealSearchWaves), true);
+        if (lane < cpr) {
+#pragma unroll
+          for (int a = 0; a < NQ; ++a)
+#pragma unroll
+            for (int vv = 0; vv < VEC; ++vv) {
+              uint32_t acc = Zt[a][7][vv];
+#pragma unroll
+              for (int kk = 6; kk >= 0; --kk) acc = gf_xtime4(acc) ^ Zt[a][kk][vv];
+              if (acc) atomicXor(&sm.red[0][a * GW + lane * VEC + vv], acc);
+            }
+        }
+        lds_signal(&sm.ready);  // the scan waves reduce red[] once every tree wave is in
+      }
     }
   } else {
     // ===================================== scan role ======================================
@@ -2001,13 +2172,17 @@ __global__ __launch_bounds__(NT) void k_query(
           for (uint32_t j0 = 0; j0 + U < rpt; j0 += U) batch(j0, rs_here, row_off + (j0 + U) * rstep);
           batch(rpt - U, rs_next, row_off);  // refills from the next tile (of this or the next query)
         }
-        for (uint32_t j0 = 0; j0 < (lane_tile ? 0u : rpt); j0 += U) {
+        // the lone query's last tile with stealing: only the first U slots statically (they were
+        // loaded at the end of the previous tile), the rest in claimed chunks (steal_tail)
+        const bool dyn = kSteal && steal_on && g + 1 == total;
+        const uint32_t rpt_g = dyn ? (uint32_t)U : rpt;
+        for (uint32_t j0 = 0; j0 < (lane_tile ? 0u : rpt_g); j0 += U) {
           // wave-uniform coefficients: lane u reads row u's (one LDS read), v_readlane broadcasts
           uint4 cf[U];
           const uint32_t gl = wi + (j0 + (lane < (uint32_t)U ? lane : 0u)) * nwg;
           uint4 c4 = load_coef<NRP>(ring, gl < ngroups ? gl : 0u);
           if (gl >= ngroups) c4 = make_uint4(0, 0, 0, 0);
-          const bool last = j0 + U == rpt;
+          const bool last = j0 + U == rpt_g;
           const uint32_t gn = last ? g + 1 : g, jn = last ? 0u : j0 + U;
           if constexpr (kM4R) {
 #pragma unroll
@@ -2065,6 +2240,10 @@ __global__ __launch_bounds__(NT) void k_query(
             __builtin_amdgcn_sched_barrier(0);
           }
         }
+        if constexpr (kSteal) {
+          static_assert(!kSteal || U == kStealU, "the scan waves' batch");
+          if (dyn) steal_trace(steal_chunks(Z, x, ring, false), false);  // x: holds nothing now
+        }
       }
       lds_signal(&sm.consumed[g % RING]);
       if (trace && sw == 0 && lane == 0 && g < 32) trace[96 + g] = wall_clock64();
@@ -2089,6 +2268,9 @@ __global__ __launch_bounds__(NT) void k_query(
           for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
             for (int v = 0; v < VEC; ++v) Z[a][kk][v] = 0;
+        if constexpr (kSteal) {
+          if (steal_on) lds_wait_geq(&sm.ready, total + (uint32_t)TW);  // the tree waves' chunks
+        }
         group_barrier(&sm.sbar, sgen, SW);  // every scan wave's planes are in red[]
         uint32_t* qslab = reinterpret_cast<uint32_t*>(slabs) + qy * slab_q_words;
         const int st = (int)threadIdx.x - TW * 64;
@@ -2119,23 +2301,22 @@ __global__ __launch_bounds__(NT) void k_query(
         }
         if (out) {
           // Fused reduce (no k_reduce launch): every scan wave's sc1 slab stores complete
-          // (vmcnt(0)) before the workgroup's ONE agent-scope counter add; the workgroup whose
-          // add comes last XORs the slabs of every workgroup with sc1 loads (the hand-off of
-          // MI355X_MICROARCH.md's first sc1 row: no L2 write-back or invalidate needed).
-          // The hand-off is also ordered by the memory model, not only by the cache flavour:
-          // release (agent) before the counter add, acquire (agent) in the last workgroup.
+          // (vmcnt(0)) before the workgroup's ONE agent-scope counter add (one lane, after the
+          // scan waves' barrier); the workgroup whose add comes last XORs the slabs of every
+          // workgroup with sc1 loads, issued after that add returned (the other scan waves: after
+          // the barrier that follows its LDS word) -- the fence-free hand-off of
+          // MI355X_MICROARCH.md's sc1 table (agent-scope atomic add row).  Round 5 dropped the
+          // release / acquire fences this hand-off does not need: each was an XCD-wide L2
+          // write-back or invalidate, 256 of them at the kernel's tail.
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           group_barrier(&sm.sbar, sgen, SW);
           const uint32_t gx = gridDim.x, xg = (uint32_t)b % red_groups;  // this slab group
           uint32_t* const cnt = qcnt + (size_t)qy * red_groups + xg;
-          if (st == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            sm.lastq = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL,
+          if (st == 0)
+            sm.lastq = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT) == gx / red_groups - 1;
-          }
           group_barrier(&sm.sbar, sgen, SW);
           if (lds_load(&sm.lastq)) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             const uint32_t words = pitch / 4, P = (uint32_t)NQ * words, nth = SW * 64;
             const uint32_t S = P >= nth ? 1u : nth / P;  // threads per output word
             for (uint32_t idx = (uint32_t)st; idx < P * S; idx += nth) {
@@ -2194,7 +2375,7 @@ hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stri
                            int p, int n, int party0, int log_parts, uint64_t prefix,
                            const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
                            uint64_t* trace, uint8_t* out, uint32_t* qcnt, uint32_t efs,
-                           uint32_t red_mode) {
+                           uint32_t red_mode, StealArgs stl) {
   uint4* fr_s = reinterpret_cast<uint4*>(scratch);
   uint32_t* fr_t = reinterpret_cast<uint32_t*>(scratch + ((size_t)qp.shape.grid.x << (kQueryKin + qp.ls)) * sizeof(uint4));
   constexpr int NRP = NQ == 1 ? 1 : (NQ == 2 ? 2 : (NQ <= 4 ? 4 : 8));
@@ -2205,7 +2386,7 @@ hipError_t query_nq(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_stri
   hipLaunchKernelGGL((k_query<NQ, NRP, VEC, UNI, TW, TILE, GY, RING, NTH>), dim3(sh.grid.x),     \
                      dim3(NTH), 0, s, d_raw, key_stride, nk, p, n, NQ, party0,                    \
                      log_parts, prefix, qp.lr, qp.lt, qp.ls, fr_s, fr_t, shard, sh.pitch, sh.cpr,  \
-                     gy, slabs, trace, out, qcnt, efs, red_mode, MpLayout{})
+                     gy, slabs, trace, out, qcnt, efs, red_mode, MpLayout{}, stl)
 #define PIR_QL(UNI, TW, GY, gy) PIR_QLN(UNI, TW, GY, gy, kFusedThreads)
   if constexpr (VEC == 2 && NQ >= 3 && NQ <= 5 && NQ > PIR_QUERY_BRANCH_MAXNQ && TILE == 1024) {
     if (sh.uniform && qp.m4r) {  // four-Russians scan waves (k_query's kM4R)
@@ -2248,7 +2429,7 @@ hipError_t query_nq_mp(const QueryPlan& qp, const uint8_t* d_key, uint32_t key_s
   hipLaunchKernelGGL((k_query<NQ, NRP, VEC, true, TW, TILE, 4, RING, NTH, true>),               \
                      dim3(sh.grid.x), dim3(NTH), 0, s, d_key, key_stride, nk, 2, n, NQ, 0,       \
                      log_parts, prefix, qp.lr, qp.lt, 0, nullptr, nullptr, shard, sh.pitch,      \
-                     sh.cpr, sh.grid.y, slabs, nullptr, nullptr, nullptr, 0u, rm, L)
+                     sh.cpr, sh.grid.y, slabs, nullptr, nullptr, nullptr, 0u, rm, L, StealArgs{})
   if constexpr (VEC == 2 && NQ >= 3 && NQ <= 5 && NQ > PIR_QUERY_BRANCH_MAXNQ && TILE == 1024) {
     if (qp.m4r) {
       PIR_QMP(kM4rTW, kM4rThreads);
@@ -2276,7 +2457,7 @@ hipError_t query_nq_mp(const QueryPlan& qp, const uint8_t* d_key, uint32_t key_s
 // parts compile in parallel.  The main object declares them extern.
 #define PIR_QNQ_ARGS                                                                            \
   (const QueryPlan&, const uint8_t*, uint32_t, int, int, int, int, int, uint64_t, const uint8_t*, \
-   uint8_t*, uint8_t*, hipStream_t, uint64_t*, uint8_t*, uint32_t*, uint32_t, uint32_t)
+   uint8_t*, uint8_t*, hipStream_t, uint64_t*, uint8_t*, uint32_t*, uint32_t, uint32_t, StealArgs)
 #define PIR_QMP_ARGS                                                                            \
   (const QueryPlan&, const uint8_t*, uint32_t, int, const MpLayout&, int, int, uint64_t,         \
    const uint8_t*, uint8_t*, hipStream_t)
@@ -2730,6 +2911,11 @@ hipError_t launch_query_mp(const QueryPlan& qp, const uint8_t* d_key, uint32_t k
 #undef PIR_QM
 }
 
+size_t query_steal_bytes(const QueryPlan& qp) {
+  const size_t nrp = qp.shape.nq == 1 ? 1 : 2;  // the rounds the stealing path serves (1-2)
+  return ((size_t)2 * qp.shape.grid.x + (size_t)qp.shape.grid.x * qp.tile * nrp / 4) * 4;
+}
+
 size_t query_scratch_bytes(const QueryPlan& qp) {
   return qp.ls ? ((size_t)qp.shape.grid.x << (kQueryKin + qp.ls)) * (sizeof(uint4) + sizeof(uint32_t)) : 0;
 }
@@ -2738,8 +2924,9 @@ hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_
                         int p, int n, int party0, int log_parts, uint64_t prefix,
                         const uint8_t* shard, uint8_t* slabs, uint8_t* scratch, hipStream_t s,
                         uint64_t* trace, uint8_t* out, uint32_t* qcnt, uint32_t efs,
-                        uint32_t red_mode) {
+                        uint32_t red_mode, StealArgs steal) {
   if (nk < 1 || (qp.ls && !scratch) || (out && !qcnt)) return hipErrorInvalidValue;
+  if (nk != 1 || !steal.buf) steal = StealArgs{};
   if (out && (red_mode < 1 || red_mode > 3 || (qp.lr < 3 && red_mode == 3))) return hipErrorInvalidValue;
   if (out && red_mode >= 2 && (efs % 4 != 0 || reinterpret_cast<uintptr_t>(out) % 4 != 0))
     return hipErrorInvalidValue;
@@ -2757,7 +2944,7 @@ hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_
     const char* tp = getenv("PIR_QUERY_TREE_PRIO");
     red_mode |= ((tp ? (uint32_t)atoi(tp) : ((nk == 1 || qp.m4r) ? 3u : 0u)) & 3u) << 8;
   }
-#define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, scratch, s, trace, out, qcnt, efs, red_mode)
+#define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, scratch, s, trace, out, qcnt, efs, red_mode, steal)
 #ifdef PIR_DEV_NQ  // development builds only (ISA / register checks): one round count
   return qp.shape.nq == PIR_DEV_NQ && qp.tile == 1024 ? PIR_Q(PIR_DEV_NQ, 1024) : hipErrorInvalidValue;
 #else

@@ -357,8 +357,8 @@ class Engine:
         """One single-launch answer of a queue of num_keys keys (at d_key, key_len apart) with
         per-workgroup phase stamps (diagnostics): an array [workgroups, 256] of microseconds
         since the earliest workgroup start (layout: pir_engine_trace_query in
-        include/pir_engine.h; 0 = stamp not reached; columns 56-57, 128-159 and 192-255 are raw
-        shader-clock ticks or counts, divided by 100 like the rest)."""
+        include/pir_engine.h; 0 = stamp not reached; columns 56-57, 59-61, 128-159 and 192-255
+        are raw shader-clock ticks or counts, divided by 100 like the rest)."""
         out = np.zeros((4096, 256), np.uint64)
         n = self._lib.pir_engine_trace_query(self._h, d_key, num_keys,
                                              out.ctypes.data_as(ctypes.c_void_p), 4096)

@@ -238,7 +238,10 @@ int pir_engine_profile_phases(pir_engine_t *e, const uint8_t *d_key, int iters, 
  * relative to the earliest start (0 = not reached): [0..6] start, key parsed, first tile root,
  * tile 0 shares ready, last tile of query 0 ready, query 0 scanned, query 0 slab written;
  * [8+d] descent level d of the first tile root (d < 32); [40+l] expansion level l of tile 0
- * (l < 16); [56], [57] shader clock (s_memtime) at start and at the first tile root; [64+g]
+ * (l < 16); [56], [57] shader clock (s_memtime) at start and at the first tile root; with
+ * end-of-query work stealing (a lone query): [58] the tree waves' last chunk folded, [59] chunks
+ * of other workgroups folded by this one's tree waves, [60] own chunks folded by the tree
+ * waves, [61] own chunks folded by the scan waves (counts, not ticks); [64+g]
  * queue tile g ready, [96+g] queue tile g consumed by scan wave 0, [128+g] shader clock at
  * [64+g] (g < 32); [160+l] expansion level l of queue tile 1 (built by the tree waves beside
  * the scan), [176] its root ready; [192+8w+k] (diagnostic builds with -DPIR_FOLD_STAMPS=1

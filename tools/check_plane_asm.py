@@ -35,30 +35,36 @@ FWD_RE = re.compile(r"^\s*s_(cbranch\w*|branch)\s+(-?\d+)\s*//\s*([0-9A-Fa-f]+):
 ADDR_RE = re.compile(r"//\s*([0-9A-Fa-f]+):")
 
 
-def disassemble(lib):
-    """Text disassembly of every gfx950 code object in lib's .hip_fatbin section (one offload
+def code_objects(lib, td):
+    """Paths (under td) of every gfx950 code object in lib's .hip_fatbin section (one offload
     bundle per translation unit, concatenated: pir_kernels.o, the pir_query_<k>.o parts, ...)."""
     magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    fat = os.path.join(td, "fatbin.bin")
+    subprocess.check_call([os.path.join(LLVM, "llvm-objcopy"), "--dump-section",
+                           f".hip_fatbin={fat}", lib, os.path.join(td, "stripped.so")])
+    data = open(fat, "rb").read()
+    starts = [m.start() for m in re.finditer(re.escape(magic), data)] + [len(data)]
+    cos = []
+    for i in range(len(starts) - 1):
+        part = os.path.join(td, f"bundle{i}.bin")
+        with open(part, "wb") as f:
+            f.write(data[starts[i]:starts[i + 1]])
+        co = os.path.join(td, f"gfx950_{i}.co")
+        r = subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle",
+                            "--type=o", f"--input={part}", f"--targets={TARGET}",
+                            f"--output={co}"], capture_output=True)
+        if r.returncode != 0 or not os.path.getsize(co):
+            continue  # a bundle without device code for this target
+        cos.append(co)
+    return cos
+
+
+def disassemble(lib):
+    """Text disassembly of every gfx950 code object in lib (code_objects)."""
     with tempfile.TemporaryDirectory() as td:
-        fat = os.path.join(td, "fatbin.bin")
-        subprocess.check_call([os.path.join(LLVM, "llvm-objcopy"), "--dump-section",
-                               f".hip_fatbin={fat}", lib, os.path.join(td, "stripped.so")])
-        data = open(fat, "rb").read()
-        starts = [m.start() for m in re.finditer(re.escape(magic), data)] + [len(data)]
-        out = []
-        for i in range(len(starts) - 1):
-            part = os.path.join(td, f"bundle{i}.bin")
-            with open(part, "wb") as f:
-                f.write(data[starts[i]:starts[i + 1]])
-            co = os.path.join(td, f"gfx950_{i}.co")
-            r = subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle",
-                                "--type=o", f"--input={part}", f"--targets={TARGET}",
-                                f"--output={co}"], capture_output=True)
-            if r.returncode != 0 or not os.path.getsize(co):
-                continue  # a bundle without device code for this target
-            out.append(subprocess.check_output([os.path.join(LLVM, "llvm-objdump"), "-d",
-                                                "--no-show-raw-insn", co], text=True))
-        return "\n".join(out)
+        return "\n".join(subprocess.check_output([os.path.join(LLVM, "llvm-objdump"), "-d",
+                                                  "--no-show-raw-insn", co], text=True)
+                         for co in code_objects(lib, td))
 
 
 def sregs(text):

@@ -63,7 +63,7 @@ for step in "$@"; do
       args=${rest#*:}
       [ "$args" = "$rest" ] && args=""
       # shellcheck disable=SC2086
-      timeout -k 10 600 python -u "tools/$script" $(plus "$args") > "${out}_${script%.py}.log" 2>&1 \
+      timeout -k 10 600 python -u "tools/$script" $(plus "$args") >> "${out}_${script%.py}.log" 2>&1 \
         || { tail -20 "${out}_${script%.py}.log"; exit 1; }
       tail -25 "${out}_${script%.py}.log"
       ;;

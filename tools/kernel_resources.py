@@ -13,20 +13,13 @@ import sys
 import tempfile
 
 sys.path.insert(0, os.path.dirname(__file__))
-from check_plane_asm import LLVM, TARGET  # noqa: E402
+from check_plane_asm import LLVM, code_objects  # noqa: E402
 
 
 def metadata(lib):
     with tempfile.TemporaryDirectory() as td:
-        fat = os.path.join(td, "fatbin.bin")
-        subprocess.check_call([os.path.join(LLVM, "llvm-objcopy"), "--dump-section",
-                               f".hip_fatbin={fat}", lib, os.path.join(td, "stripped.so")])
-        co = os.path.join(td, "gfx950.co")
-        subprocess.check_call([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle",
-                               "--type=o", f"--input={fat}", f"--targets={TARGET}",
-                               f"--output={co}"])
-        return subprocess.check_output([os.path.join(LLVM, "llvm-readelf"), "--notes", co],
-                                       text=True)
+        return "\n".join(subprocess.check_output([os.path.join(LLVM, "llvm-readelf"), "--notes", co],
+                                                 text=True) for co in code_objects(lib, td))
 
 
 def main():

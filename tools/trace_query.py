@@ -56,8 +56,21 @@ def main():
             print(f"  xcd {x}: last_tile_ready med {np.median(tr[m, il]):8.1f}  end med {np.median(tr[m, ie]):8.1f}"
                   f" (min {tr[m, ie].min():8.1f} max {tr[m, ie].max():8.1f})  clock med {np.median(ghz[m]):.3f} GHz")
         print(f"  corr(end, clock) over workgroups: {np.corrcoef(tr[:, ie], ghz)[0, 1]:+.2f}")
+        # end-of-query work stealing (a lone query): chunk counts are raw (not ticks)
+        cnt = np.rint(raw[:, 59:62]).astype(np.int64)
+        if cnt.any():
+            print(f"  stealing: chunks of others folded by tree waves {cnt[:, 0].sum()} "
+                  f"(max {cnt[:, 0].max()}/wg), own by tree waves {cnt[:, 1].sum()}, own by scan "
+                  f"waves {cnt[:, 2].sum()}; tree waves done med {np.median(tr[:, 58]):.1f} "
+                  f"max {tr[:, 58].max():.1f} us")
+        print(f"  end spread: med {np.median(tr[:, ie]):.1f}  p90 {np.percentile(tr[:, ie], 90):.1f}"
+              f"  max {tr[:, ie].max():.1f} us")
+        rd = [med[64 + g] for g in range(32) if tr[:, 64 + g].all()]
+        cs = [med[96 + g] for g in range(32) if tr[:, 96 + g].all()]
+        if a.queue == 1 and len(rd) > 1:
+            print("  tile ready    (med us):", " ".join(f"{v:.1f}" for v in rd))
+            print("  tile consumed (med us):", " ".join(f"{v:.1f}" for v in cs))
         if a.queue > 1:
-            rd = [med[64 + g] for g in range(32) if tr[:, 64 + g].all()]
             cs = [med[96 + g] for g in range(32) if tr[:, 96 + g].all()]
             print("  queue tile ready    (med us):", " ".join(f"{v:.0f}" for v in rd))
             print("  queue tile consumed (med us):", " ".join(f"{v:.0f}" for v in cs))
