@@ -54,7 +54,7 @@ for step in "$@"; do
       args=${rest#*:}
       [ "$args" = "$rest" ] && args=""
       # shellcheck disable=SC2086
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "${out}_prof_${name}" -o run \
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "${out}_prof_${name}" -o run --output-format csv \
         -- python3 -u bench.py $(plus "$args") > "${out}_prof_${name}.log" 2>&1 \
         || { tail -20 "${out}_prof_${name}.log"; exit 1; }
       ;;
