@@ -324,18 +324,74 @@ __device__ __forceinline__ void aes_ctr_rowk(const Tab& T, const uint4 (&key)[NK
   }
 }
 
-// Row shape, one block with counter `ctr` (generic helper, e.g. key generation).
+// 20 LDS lookups as one group (the row-shape round: the key schedule's 4 + the state's 16), as
+// lds_read8 below for the column shape.  `a` are LDS byte addresses.
+__device__ __forceinline__ void lds_read20(uint32_t (&v)[20], const uint32_t (&a)[20]) {
+  asm volatile(
+      "ds_read_b32 %0, %20\n\t" "ds_read_b32 %1, %21\n\t" "ds_read_b32 %2, %22\n\t"
+      "ds_read_b32 %3, %23\n\t" "ds_read_b32 %4, %24\n\t" "ds_read_b32 %5, %25\n\t"
+      "ds_read_b32 %6, %26\n\t" "ds_read_b32 %7, %27\n\t" "ds_read_b32 %8, %28\n\t"
+      "ds_read_b32 %9, %29\n\t" "ds_read_b32 %10, %30\n\t" "ds_read_b32 %11, %31\n\t"
+      "ds_read_b32 %12, %32\n\t" "ds_read_b32 %13, %33\n\t" "ds_read_b32 %14, %34\n\t"
+      "ds_read_b32 %15, %35\n\t" "ds_read_b32 %16, %36\n\t" "ds_read_b32 %17, %37\n\t"
+      "ds_read_b32 %18, %38\n\t" "ds_read_b32 %19, %39\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]),
+        "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]),
+        "=&v"(v[12]), "=&v"(v[13]), "=&v"(v[14]), "=&v"(v[15]), "=&v"(v[16]), "=&v"(v[17]),
+        "=&v"(v[18]), "=&v"(v[19])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]),
+        "v"(a[8]), "v"(a[9]), "v"(a[10]), "v"(a[11]), "v"(a[12]), "v"(a[13]), "v"(a[14]),
+        "v"(a[15]), "v"(a[16]), "v"(a[17]), "v"(a[18]), "v"(a[19])
+      : "memory");
+}
+
+// Row shape, one block with counter `ctr` (k_query's 3-lanes-per-node levels, key generation).
+// Per round the key schedule's 4 S-box lookups (from the previous round key) and the state's
+// 16 T-box lookups (from the previous state) go out as one group (lds_read20): one LDS round
+// trip per round where the compiler, at k_query's register limit, issued a few at a time.
 __device__ __forceinline__ uint4 aes_ctr_block(const Tab& T, uint4 key, uint32_t ctr) {
+  const uint32_t lb = (uint32_t)(uintptr_t)T.base;  // LDS byte address (see aes_col)
   uint32_t k0 = key.x, k1 = key.y, k2 = key.z, k3 = key.w;
-  uint32_t w0 = k0, w1 = k1, w2 = k2, w3 = k3 ^ (ctr << 24);
+  uint32_t w[4] = {k0, k1, k2, k3 ^ (ctr << 24)};
 #pragma unroll
-  for (int r = 0; r < 9; ++r) {
-    key_next(T, k0, k1, k2, k3, kRcon[r]);
-    round_row(T, w0, w1, w2, w3, rotr8(k0), rotr8(k1), rotr8(k2), rotr8(k3));
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t p1 = k0 ^ k1, p2 = p1 ^ k2, p3 = p2 ^ k3;  // the word chain, old key
+    uint32_t ad[20], v[20];
+    ad[0] = lb + tab_addr<1>(k3, T.l2);  // SubWord(RotWord(k3)): S in byte 0..3
+    ad[1] = lb + tab_addr<2>(k3, T.l0);
+    ad[2] = lb + tab_addr<3>(k3, T.l0);
+    ad[3] = lb + tab_addr<0>(k3, T.l2);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t a0 = w[c], a1 = w[(c + 1) & 3], a2 = w[(c + 2) & 3], a3 = w[(c + 3) & 3];
+      if (r < 9) {  // round_row's column c
+        ad[4 + 4 * c] = lb + tab_addr<0>(a0, T.l0);
+        ad[5 + 4 * c] = lb + tab_addr<2>(a2, T.l2);
+        ad[6 + 4 * c] = lb + tab_addr<1>(a1, T.l0);
+        ad[7 + 4 * c] = lb + tab_addr<3>(a3, T.l2);
+      } else {  // last_col's S-box bytes
+        ad[4 + 4 * c] = lb + tab_addr<0>(a0, T.l2);
+        ad[5 + 4 * c] = lb + tab_addr<1>(a1, T.l0);
+        ad[6 + 4 * c] = lb + tab_addr<2>(a2, T.l0);
+        ad[7 + 4 * c] = lb + tab_addr<3>(a3, T.l2);
+      }
+    }
+    lds_read20(v, ad);
+    const uint32_t t = ((v[0] & 0xffu) | (v[1] & 0xff00u) | (v[2] & 0xff0000u) |
+                        (v[3] & 0xff000000u)) ^ kRcon[r];
+    k0 ^= t; k1 = p1 ^ t; k2 = p2 ^ t; k3 = p3 ^ t;
+    const uint32_t kk[4] = {k0, k1, k2, k3};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (r < 9)
+        w[c] = xor3(v[4 + 4 * c], v[5 + 4 * c], rotl8(xor3(v[6 + 4 * c], v[7 + 4 * c], rotr8(kk[c]))));
+      else
+        w[c] = ((v[4 + 4 * c] & 0xffu) | (v[5 + 4 * c] & 0xff00u) | (v[6 + 4 * c] & 0xff0000u) |
+                (v[7 + 4 * c] & 0xff000000u)) ^ kk[c];
+    }
   }
-  key_next(T, k0, k1, k2, k3, kRcon[9]);
-  return make_uint4(last_col(T, w0, w1, w2, w3, k0), last_col(T, w1, w2, w3, w0, k1),
-                    last_col(T, w2, w3, w0, w1, k2), last_col(T, w3, w0, w1, w2, k3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // ---- column shape: 4 lanes (a DPP quad) per block, lane q = column q ----------------------
@@ -350,25 +406,69 @@ constexpr int kQ3333 = 0xFF;  // lane 3
 constexpr int kQ0012 = 0x90;  // q-1 (lane 0 reads itself)
 constexpr int kQ0101 = 0x44;  // q-2 (lanes 0,1 read themselves)
 
+// The 8 LDS lookups of a column-shape round as ONE group (one LDS round trip): left to itself,
+// the scheduler of a kernel at its register limit (k_query: 128 VGPRs) issued them as three
+// dependent batches -- the state's 4, then the key schedule's 2 + 2 -- so a tile-root descent
+// level took ≈3 600 cycles against ≈2 000 for the same code in a register-rich kernel
+// (tools/micro/aes_col_latency.hip; the k_query disassembly).  `a` are LDS byte addresses.
+__device__ __forceinline__ void lds_read8(uint32_t (&v)[8], const uint32_t (&a)[8]) {
+  asm volatile(
+      "ds_read_b32 %0, %8\n\t"
+      "ds_read_b32 %1, %9\n\t"
+      "ds_read_b32 %2, %10\n\t"
+      "ds_read_b32 %3, %11\n\t"
+      "ds_read_b32 %4, %12\n\t"
+      "ds_read_b32 %5, %13\n\t"
+      "ds_read_b32 %6, %14\n\t"
+      "ds_read_b32 %7, %15\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]),
+        "=&v"(v[6]), "=&v"(v[7])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7])
+      : "memory");
+}
+
 // AES-128_k(pt) where lane q holds key word k_q and plaintext word pt_q; returns ciphertext
 // word q.  All 4 lanes of the quad must be active.  mq1/mq2: all-ones when q >= 1 / q >= 2.
+// Per round the key schedule's 4 S-box lookups (from the previous round key) and the state's 4
+// T-box lookups (from the previous state) go out together (lds_read8); the schedule's prefix XOR
+// (two DPP steps on the previous key) runs while they are in flight.
 __device__ __forceinline__ uint32_t aes_col(const Tab& T, uint32_t kq, uint32_t ptq, uint32_t mq1,
                                             uint32_t mq2) {
+  // LDS byte address of the table: the low 32 bits of the generic address (the shared
+  // aperture's base has zero low bits)
+  const uint32_t lb = (uint32_t)(uintptr_t)T.base;
   uint32_t w = kq ^ ptq;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     // key schedule: k'_q = SubWordRot(k3) ^ rcon ^ (k_0 ^ ... ^ k_q)
     const uint32_t k3 = qperm<kQ3333>(kq);
-    const uint32_t t = (T.t2<1>(k3) & 0xffu) | (T.t0<2>(k3) & 0xff00u) |
-                       (T.t0<3>(k3) & 0xff0000u) | (T.t2<0>(k3) & 0xff000000u);
     uint32_t pre = kq ^ (qperm<kQ0012>(kq) & mq1);
     pre ^= qperm<kQ0101>(pre) & mq2;
-    kq = xor3(pre, t, kRcon[r]);
     const uint32_t b = qperm<kQ1230>(w), c = qperm<kQ2301>(w), d = qperm<kQ3012>(w);
+    uint32_t ad[8], v[8];
+    ad[0] = lb + tab_addr<1>(k3, T.l2);  // Te2[byte 1]: S in byte 0
+    ad[1] = lb + tab_addr<2>(k3, T.l0);                // Te0[byte 2]: S in byte 1
+    ad[2] = lb + tab_addr<3>(k3, T.l0);                // Te0[byte 3]: S in byte 2
+    ad[3] = lb + tab_addr<0>(k3, T.l2);                // Te2[byte 0]: S in byte 3
+    if (r < 9) {
+      ad[4] = lb + tab_addr<0>(w, T.l0);
+      ad[5] = lb + tab_addr<2>(c, T.l2);
+      ad[6] = lb + tab_addr<1>(b, T.l0);
+      ad[7] = lb + tab_addr<3>(d, T.l2);
+    } else {  // last round (last_col): S-box bytes only
+      ad[4] = lb + tab_addr<0>(w, T.l2);
+      ad[5] = lb + tab_addr<1>(b, T.l0);
+      ad[6] = lb + tab_addr<2>(c, T.l0);
+      ad[7] = lb + tab_addr<3>(d, T.l2);
+    }
+    lds_read8(v, ad);
+    const uint32_t t = (v[0] & 0xffu) | (v[1] & 0xff00u) | (v[2] & 0xff0000u) | (v[3] & 0xff000000u);
+    kq = xor3(pre, t, kRcon[r]);
     if (r < 9)
-      w = xor3(T.t0<0>(w), T.t2<2>(c), rotl8(xor3(T.t0<1>(b), T.t2<3>(d), rotr8(kq))));
+      w = xor3(v[4], v[5], rotl8(xor3(v[6], v[7], rotr8(kq))));
     else
-      w = last_col(T, w, b, c, d, kq);
+      w = ((v[4] & 0xffu) | (v[5] & 0xff00u) | (v[6] & 0xff0000u) | (v[7] & 0xff000000u)) ^ kq;
   }
   return w;
 }
