@@ -56,3 +56,42 @@ def test_four_russians_checker_flags_problems():
     assert any("foreign" in p for _, p in M.check("\n".join(foreign))[0])
     spill = good[:1] + ["\tv_writelane_b32 v100, s5, 3"] + good[1:]
     assert any("spill" in p for _, p in M.check("\n".join(spill))[0])
+
+
+def _aes_round_groups(asm):
+    """For every column-shape AES round in k_query (its key-schedule broadcast `quad_perm:
+    [3,3,3,3]`), the number of ds_read_b32 issued between that round's first lookup and the
+    s_waitcnt that ends them (pir_aes.h aes_col: all 8 as one group)."""
+    import re
+    out = []
+    fn = None
+    lines = asm.split("\n")
+    for i, ln in enumerate(lines):
+        m = re.match(r"[0-9a-f]{16} <(\S+)>:", ln)
+        if m:
+            fn = m.group(1)
+            continue
+        if fn is None or "k_query" not in fn or "quad_perm:[3,3,3,3]" not in ln:
+            continue
+        n, seen = 0, False
+        for ln2 in lines[i + 1:i + 80]:
+            s = ln2.strip()
+            if s.startswith("ds_read_b32"):
+                n += 1
+                seen = True
+            elif seen and s.startswith("s_waitcnt") and "lgkmcnt" in s:
+                break
+        out.append((fn, n))
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libpir_engine.so not built")
+def test_column_aes_rounds_issue_one_lookup_group():
+    """k_query's column-shape AES (tile-root descent, narrow tile levels) issues each round's 8
+    LDS lookups -- the key schedule's 4 and the state's 4 -- as ONE group before a single wait
+    (round 5: the compiler had split them into 3 dependent batches at 128 VGPRs)."""
+    import check_plane_asm as C
+    groups = _aes_round_groups(C.disassemble(LIB))
+    assert len(groups) > 100, "no column-shape AES rounds found in k_query"
+    bad = [(f, n) for f, n in groups if n != 8]
+    assert not bad, f"{len(bad)} of {len(groups)} rounds split: {bad[:5]}"
