@@ -15,6 +15,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <string>
@@ -1095,14 +1097,91 @@ int gather_threads() {
   return std::max(1, std::min(8, n));
 }
 
-// fn(t, T) on T host threads (t = 0 on the caller's)
-template <class F>
-void parallel_run(int T, const F& fn) {
-  std::vector<std::thread> th;
-  th.reserve((size_t)T - 1);
-  for (int t = 1; t < T; ++t) th.emplace_back([&fn, t, T] { fn(t, T); });
-  fn(0, T);
-  for (auto& x : th) x.join();
+// T - 1 host threads kept for the length of one staged copy (a 64 GiB setup is ~1000 chunks:
+// spawning a thread team per chunk cost more than some chunks' copies); run(fn) calls fn(t, T)
+// on every thread, the caller's as t = 0, and returns when all have.
+class Crew {
+ public:
+  explicit Crew(int T) : T_(T) {
+    for (int t = 1; t < T_; ++t) th_.emplace_back([this, t] { loop(t); });
+  }
+  ~Crew() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      quit_ = true;
+    }
+    go_.notify_all();
+    for (auto& x : th_) x.join();
+  }
+  void run(const std::function<void(int, int)>& fn) {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      job_ = &fn;
+      pending_ = T_ - 1;
+      ++gen_;
+    }
+    go_.notify_all();
+    fn(0, T_);
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [this] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop(int t) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int, int)>* job;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        go_.wait(lk, [&] { return quit_ || gen_ != seen; });
+        if (quit_) return;
+        seen = gen_;
+        job = job_;
+      }
+      (*job)(t, T_);
+      std::lock_guard<std::mutex> lk(m_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  const int T_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable go_, done_;
+  const std::function<void(int, int)>* job_ = nullptr;
+  uint64_t gen_ = 0;
+  int pending_ = 0;
+  bool quit_ = false;
+};
+
+// [a, b) of n items split into T contiguous slices: slice t
+inline void slice_of(uint64_t n, int t, int T, uint64_t& a, uint64_t& b) {
+  a = n * (uint64_t)t / (uint64_t)T;
+  b = n * (uint64_t)(t + 1) / (uint64_t)T;
+}
+
+// dst + i * efs <- rows[i] for i in [a, b), each run of rows that lie back to back in host
+// memory (the shim's client files and indexList rows are one block) as one memcpy
+inline void gather_rows(uint8_t* dst, const uint8_t* const* rows, uint64_t a, uint64_t b,
+                        uint32_t efs) {
+  for (uint64_t i = a; i < b;) {
+    const uint8_t* s0 = rows[i];
+    uint64_t j = i + 1;
+    while (j < b && rows[j] == s0 + (j - i) * efs) ++j;
+    memcpy(dst + i * efs, s0, (size_t)(j - i) * efs);
+    i = j;
+  }
+}
+// the reverse: rows[i] <- src + i * efs
+inline void scatter_rows(uint8_t* const* rows, const uint8_t* src, uint64_t a, uint64_t b,
+                         uint32_t efs) {
+  for (uint64_t i = a; i < b;) {
+    uint8_t* d0 = rows[i];
+    uint64_t j = i + 1;
+    while (j < b && rows[j] == d0 + (j - i) * efs) ++j;
+    memcpy(d0, src + i * efs, (size_t)(j - i) * efs);
+    i = j;
+  }
 }
 
 // Host rows -> device through two pinned staging buffers of `chunk_bytes`: chunk c is gathered
@@ -1116,7 +1195,7 @@ int staged_h2d(pir_engine* e, uint64_t nchunks, size_t chunk_bytes, const Fill& 
   if (!nchunks) return PIR_OK;
   uint8_t* h[2] = {nullptr, nullptr};
   hipEvent_t done[2] = {nullptr, nullptr};
-  const int T = gather_threads();
+  Crew crew(gather_threads());
   int rc = PIR_OK;
   for (int i = 0; i < 2 && !rc; ++i) {
     if (hipHostMalloc(&h[i], chunk_bytes) != hipSuccess ||
@@ -1129,7 +1208,8 @@ int staged_h2d(pir_engine* e, uint64_t nchunks, size_t chunk_bytes, const Fill& 
       rc = fail(PIR_EHIP, "staged upload: chunk %llu", (unsigned long long)(c - 2));
       break;
     }
-    parallel_run(T, [&](int t, int nt) { fill(c, h[b], t, nt); });
+    const std::function<void(int, int)> job = [&](int t, int nt) { fill(c, h[b], t, nt); };
+    crew.run(job);
     hipError_t err = issue(c, h[b], e->stream);
     if (err == hipSuccess) err = hipEventRecord(done[b], e->stream);
     if (err != hipSuccess) rc = fail(PIR_EHIP, "staged upload: %s", hipGetErrorString(err));
@@ -1162,8 +1242,9 @@ int pir_engine_set_shard_rows(pir_engine_t* e, const uint8_t* const* rows, uint6
       e, (nrows + m - 1) / m, (size_t)m * efs,
       [&](uint64_t c, uint8_t* dst, int t, int nt) {
         const uint64_t r0 = c * m, n = std::min(m, nrows - r0);
-        for (uint64_t i = (uint64_t)t; i < n; i += (uint64_t)nt)
-          memcpy(dst + i * efs, rows[r0 + i], efs);
+        uint64_t a, b;
+        slice_of(n, t, nt, a, b);
+        gather_rows(dst, rows + r0, a, b, efs);
       },
       [&](uint64_t c, const uint8_t* src, hipStream_t s) {
         const uint64_t r0 = c * m, n = std::min(m, nrows - r0);
@@ -1197,7 +1278,7 @@ int pir_engine_get_shard_rows(pir_engine_t* e, uint8_t* const* rows, uint64_t ro
     return err;
   };
   if (!rc && nchunks && enqueue(0) != hipSuccess) rc = fail(PIR_EHIP, "get_shard_rows: copy");
-  const int T = gather_threads();
+  Crew crew(gather_threads());
   for (uint64_t c = 0; c < nchunks && !rc; ++c) {
     if (hipEventSynchronize(ready[c & 1]) != hipSuccess) {
       rc = fail(PIR_EHIP, "get_shard_rows: chunk %llu", (unsigned long long)c);
@@ -1209,9 +1290,12 @@ int pir_engine_get_shard_rows(pir_engine_t* e, uint8_t* const* rows, uint64_t ro
     }
     const uint64_t r0 = c * m, n = std::min(m, nrows - r0);
     const uint8_t* src = h[c & 1];
-    parallel_run(T, [&](int t, int nt) {
-      for (uint64_t i = (uint64_t)t; i < n; i += (uint64_t)nt) memcpy(rows[r0 + i], src + i * efs, efs);
-    });
+    const std::function<void(int, int)> job = [&](int t, int nt) {
+      uint64_t a, b;
+      slice_of(n, t, nt, a, b);
+      scatter_rows(rows + r0, src, a, b, efs);
+    };
+    crew.run(job);
   }
   (void)hipStreamSynchronize(e->stream);
   for (int i = 0; i < 2; ++i) {
@@ -1277,12 +1361,17 @@ int pir_engine_encode_across_rows(pir_engine_t* e, const uint8_t* const* files, 
         e, nchunks, sbytes,
         [&](uint64_t c, uint8_t* dst, int t, int nt) {
           const uint64_t r0 = c * m, n = std::min(m, e->rows - r0), tot = (uint64_t)k * n;
-          for (uint64_t i = (uint64_t)t; i < tot; i += (uint64_t)nt) {
-            const uint64_t j = i / n, r = i - j * n;
-            const uint64_t src = encdb * j + prow0 + r0 + r;
-            uint8_t* d = dst + (j * n + r) * efs;
-            if (src < num_files) memcpy(d, files[src], efs);
-            else memset(d, 0, efs);
+          uint64_t a, b;
+          slice_of(tot, t, nt, a, b);  // items i = j n + r: block j, row r
+          while (a < b) {
+            const uint64_t j = a / n, r = a - j * n, e_r = std::min(n, r + (b - a));  // rows [r, e_r) of block j
+            const uint64_t f0 = encdb * j + prow0 + r0;  // the file of row 0 of block j
+            uint8_t* d = dst + j * n * efs;
+            const uint64_t live = f0 + e_r <= num_files ? e_r : (f0 >= num_files ? 0 : num_files - f0);
+            if (live > r) gather_rows(d, files + f0, r, live, efs);
+            const uint64_t z0 = std::max(r, live);
+            if (e_r > z0) memset(d + z0 * efs, 0, (size_t)(e_r - z0) * efs);
+            a += e_r - r;
           }
         },
         [&](uint64_t c, const uint8_t* src, hipStream_t s) {
@@ -1327,8 +1416,13 @@ int pir_engine_encode_within_rows(pir_engine_t* e, const uint8_t* const* files, 
         e, nchunks, sbytes,
         [&](uint64_t c, uint8_t* dst, int t, int nt) {
           const uint64_t r0 = c * m, n = std::min(m, e->rows - r0), nf = nfiles_of(r0, n);
-          for (uint64_t i = (uint64_t)t; i < nf; i += (uint64_t)nt)
-            memcpy(dst + i * fb, files[prow0 + r0 + i], file_bytes);
+          uint64_t a, b;
+          slice_of(nf, t, nt, a, b);
+          if (file_bytes == fb) {
+            gather_rows(dst, files + prow0 + r0, a, b, fb);
+          } else {
+            for (uint64_t i = a; i < b; ++i) memcpy(dst + i * fb, files[prow0 + r0 + i], file_bytes);
+          }
         },
         [&](uint64_t c, const uint8_t* src, hipStream_t s) {
           const uint64_t r0 = c * m, n = std::min(m, e->rows - r0), nf = nfiles_of(r0, n);
