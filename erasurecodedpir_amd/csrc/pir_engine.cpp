@@ -175,7 +175,8 @@ struct pir_engine {
   hipEvent_t* ev = nullptr;  // the current answer's slot (nullptr: profiling off)
   // the engine's work buffers (slabs, tree nodes, share buffers, staged keys) are shared by
   // every answer: an answer enqueued on a stream other than the previous answer's waits for
-  // that answer's last use of them (ev_ws, recorded after every answer)
+  // that answer's last use of them (ev_ws: recorded after an answer on a caller's stream, and
+  // for the engine's own stream when the next answer comes on another one)
   hipEvent_t ev_ws = nullptr;
   hipStream_t ws_stream = nullptr;
   // RCCL
@@ -569,16 +570,24 @@ int check_comm(const pir_engine* e) {
                         : PIR_OK;
 }
 
-// before an answer on stream s: order it after the previous answer's use of the workspace
+// before an answer on stream s: order it after the previous answer's use of the workspace.
+// The engine's own stream records that answer's event only now, when another stream needs it
+// (everything enqueued on it so far, the previous answer included): an event record between
+// two launches on one stream delays the second by ~5.6 us of dispatch (the lone-query gap of
+// profiles/r05/r5af_lone_gaps_depth4_depth16.txt; tools/micro/dispatch_gap.hip, mode 7).  A
+// caller's stream records at release, while it is known to exist.
 int ws_acquire(pir_engine* e, hipStream_t s) {
   if (int rc = check_comm(e)) return rc;
-  if (e->ws_stream && e->ws_stream != s) HIP_TRY(hipStreamWaitEvent(s, e->ev_ws, 0));
+  if (e->ws_stream && e->ws_stream != s) {
+    if (e->ws_stream == e->stream) HIP_TRY(hipEventRecord(e->ev_ws, e->stream));
+    HIP_TRY(hipStreamWaitEvent(s, e->ev_ws, 0));
+  }
   return PIR_OK;
 }
 // after it: the next answer, on whatever stream, waits for this one
 int ws_release(pir_engine* e, hipStream_t s, int rc) {
   if (rc) return rc;
-  HIP_TRY(hipEventRecord(e->ev_ws, s));
+  if (s != e->stream) HIP_TRY(hipEventRecord(e->ev_ws, s));
   e->ws_stream = s;
   return PIR_OK;
 }
