@@ -185,7 +185,10 @@ int pir_engine_cd_key_len(int p, int n, int t, int num_cd_keys_needed, int num_c
 int pir_engine_eval_all(pir_engine_t *e, const uint8_t *key, uint8_t *out);
 
 /* ---- answers, device-resident (asynchronous on `stream`, a hipStream_t or NULL for the
- *      engine's own stream) ---- */
+ *      engine's own stream).  Answers share the engine's work buffers: one enqueued on a
+ *      different stream than the previous answer waits on the device for that answer (an
+ *      event recorded on the previous stream; answers that stay on one stream record none, so
+ *      back-to-back launches there carry no event-record dispatch gap). ---- */
 int pir_engine_answer_dev(pir_engine_t *e, const uint8_t *d_key, uint8_t *d_result,
                           void *stream);
 /* `num_keys` keys of key_len bytes back to back; results num_keys x num_rounds x record_bytes.
