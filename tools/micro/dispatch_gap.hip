@@ -13,6 +13,7 @@
 //   6: mode 2 with an 80-B private segment
 //   7: mode 0 with a hipEventRecord after each small kernel (pir_engine's ws_release)
 //   8: mode 0 with a hipStreamWaitEvent on an already-complete event before each big kernel
+//   9: mode 1 with the private segment never touched at run time
 // Build: hipcc -O3 --offload-arch=gfx950 -o dispatch_gap dispatch_gap.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -74,6 +75,20 @@ __global__ __launch_bounds__(256) void k_big_plain_scratch(uint32_t* out, uint32
   if (loc[k & 15] == 0x9e3779b9u) out[blockIdx.x] = 1;
 }
 
+// an 80-B private segment that no lane touches at run time (k != 12345 in every launch)
+__global__ __launch_bounds__(1024) void k_big_lds_scratch_cold(uint32_t* out, uint32_t us, uint32_t k) {
+  __shared__ uint32_t lds[24 * 1024];
+  lds[threadIdx.x] = threadIdx.x;
+  if (k == 12345u) {
+    volatile uint32_t loc[16];
+    for (int i = 0; i < 16; ++i) loc[i] = threadIdx.x + i;
+    lds[threadIdx.x] = loc[(threadIdx.x + k) & 15];
+  }
+  __syncthreads();
+  spin(us);
+  if (lds[(threadIdx.x + 1) & 1023] == 0x9e3779b9u) out[blockIdx.x] = 1;
+}
+
 __global__ __launch_bounds__(256) void k_big_plain(uint32_t* out, uint32_t us) {
   spin(us);
   if (threadIdx.x == 0 && out[blockIdx.x] == 0x9e3779b9u) out[blockIdx.x] = 1;
@@ -89,10 +104,11 @@ int main() {
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   hipEvent_t ev;
   CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-  for (int mode = 0; mode < 9; ++mode) {
+  for (int mode = 0; mode < 10; ++mode) {
     for (int r = 0; r < 40; ++r) {
       if (mode == 8) CK(hipStreamWaitEvent(s, ev, 0));
-      if (mode == 0 || mode >= 7) hipLaunchKernelGGL(k_big_lds, dim3(cus), dim3(1024), 0, s, out, 20u);
+      if (mode == 9) hipLaunchKernelGGL(k_big_lds_scratch_cold, dim3(cus), dim3(1024), 0, s, out, 20u, (uint32_t)r);
+      if (mode == 0 || mode == 7 || mode == 8) hipLaunchKernelGGL(k_big_lds, dim3(cus), dim3(1024), 0, s, out, 20u);
       if (mode == 1) hipLaunchKernelGGL(k_big_lds_scratch, dim3(cus), dim3(1024), 0, s, out, 20u, (uint32_t)r);
       if (mode == 2) hipLaunchKernelGGL(k_big_plain, dim3(cus), dim3(256), 0, s, out, 20u);
       if (mode == 5) hipLaunchKernelGGL(k_big_lds_scratch16, dim3(cus), dim3(1024), 0, s, out, 20u, (uint32_t)r);
