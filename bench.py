@@ -522,6 +522,94 @@ def r5(x):
     return round(float(x), 5)
 
 
+def trace_stats(eng, keys, nk):
+    """One traced k_query launch (pir_engine_trace_query: per-workgroup wall-clock stamps and
+    s_memtime shader-clock stamps) of a queue of nk of `keys`, after the timed legs: the shader
+    clock this box ran the kernel at (s_memtime ticks between the first and last stamped tile
+    over the 100 MHz wall clock between them, median over workgroups) and, for the first query,
+    when tile 0 was ready (the head before the first row can be folded).  None when the shape
+    does not run k_query."""
+    nk = max(1, min(nk, len(keys)))
+    kl = eng.key_len
+    try:
+        d = eng.alloc_dev(kl * nk)
+        try:
+            eng.h2d(d, b"".join(keys[:nk]))
+            tr = eng.trace_query(d, nk)
+        finally:
+            eng.free_dev(d)
+    except Exception:  # noqa: BLE001 - shape without k_query, or no trace support
+        return None
+    if not len(tr):
+        return None
+    raw = tr * 100.0  # wall stamps back to 100 MHz ticks; shader-clock columns back to ticks
+    g = [i for i in range(32) if tr[:, 64 + i].all() and tr[:, 128 + i].all()]
+    if len(g) >= 2:
+        ghz = (raw[:, 128 + g[-1]] - raw[:, 128 + g[0]]) / ((tr[:, 64 + g[-1]] - tr[:, 64 + g[0]]) * 1e3)
+        span = f"tiles {g[0]}..{g[-1]} of a traced queue of {nk} queries"
+    else:
+        ghz = (raw[:, 57] - raw[:, 56]) / ((tr[:, 2] - tr[:, 0]) * 1e3)
+        span = "start -> first tile root of one traced query"
+    ghz = ghz[np.isfinite(ghz) & (ghz > 0)]
+    return {"shader_clock_ghz": {"median": round(float(np.median(ghz)), 3),
+                                 "min": round(float(ghz.min()), 3), "max": round(float(ghz.max()), 3),
+                                 "source": "k_query s_memtime vs 100 MHz wall-clock stamps, " + span},
+            "tile0_ready_us_median": round(float(np.median(tr[:, 3])), 2),
+            "first_tile_root_us_median": round(float(np.median(tr[:, 2])), 2),
+            "launch_end_us_max": round(float(tr[:, 6].max()), 2)}
+
+
+def _pmc_issue(config, queries_per_launch, kern_ms, clock_ghz):
+    """Issue-port ceilings of a compute-bound k_query from its committed, sha-stamped counters
+    (profiles/pmc_<config>.json: SQ_INSTS_SALU / SQ_INSTS_VALU per launch): the share of the
+    CUs' scalar issue (1 SALU per CU-clock) and vector issue (0.5 VALU per SIMD-clock, 4 SIMDs)
+    this run's kernel time implies, at the clock this run measured (else the counters' implied
+    clock).  None unless the counters describe the loaded library."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if not _pmc_current(d) or not kern_ms or kern_ms != kern_ms:
+        return None
+    c = d.get("counters_per_launch", {})
+    q_prof = d.get("queries_per_launch", queries_per_launch)
+    f = clock_ghz or d.get("issue", {}).get("shader_clock_GHz_implied")
+    if not f or not c.get("SQ_INSTS_SALU"):
+        return None
+    cyc = kern_ms / 1e3 * f * 1e9  # CU clocks of this run's launch
+    salu = c["SQ_INSTS_SALU"] / q_prof * queries_per_launch
+    valu = c.get("SQ_INSTS_VALU", 0) / q_prof * queries_per_launch
+    return {"salu_issue_frac": round(salu / (256 * cyc), 4),
+            "valu_issue_frac": round(valu / (256 * 4 * 0.5 * cyc), 4),
+            "salu_insts_per_query": int(salu / queries_per_launch),
+            "valu_insts_per_query": int(valu / queries_per_launch),
+            "clock_ghz_used": round(f, 3),
+            "clock_source": "this run's k_query stamps" if clock_ghz else "counters' implied clock",
+            "source": f"profiles/pmc_{config}.json (SQ_INSTS_SALU / SQ_INSTS_VALU per launch, "
+                      "sha-stamped at this library)"}
+
+
+def single_phases(ph, ms_per_query):
+    """The per-query phases of a lone answer, from the profiled pass (HIP events on the engine
+    stream).  On the k_query path (fused == 2) key parse, tree and scan are ONE kernel, so the
+    phases are what exists: launch (answer start -> k_query start), k_query, k_reduce, and the
+    exchange / tail; they sum to the profiled answer, quoted beside the unprofiled ms_per_query
+    (the two runs differ by the profiling events' own dispatch cost)."""
+    if ph.get("fused") == 2.0:
+        names = {"launch": "launch", "scan": "k_query", "reduce": "k_reduce",
+                 "comm_fold": "exchange_and_tail"}
+        phases = {names[k]: r5(ph[k]) for k in names if k in ph}
+        total = ph.get("total", sum(phases.values()))
+        return {"phases_ms": phases, "phases_sum_ms": r5(sum(phases.values())),
+                "profiled_ms_per_query": r5(total),
+                "phases_sum_over_ms_per_query": round(sum(phases.values()) / ms_per_query, 4)
+                if ms_per_query else None,
+                "phases_path": "k_query (key parse + DPF tree + scan in one launch) + k_reduce"}
+    return {"phases_ms": {k: r5(v) for k, v in ph.items() if k not in ("chunks", "fused")},
+            "phases_path": "multi-kernel (k_frontier / k_expand / k_fused or k_scan) + k_reduce"}
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--cpu-worker":
         return _cpu_worker(sys.argv[2:])
@@ -628,6 +716,9 @@ def main():
     path = {2.0: "k_query", 1.0: "k_fused", 0.0: "k_expand+k_scan"}.get(ph.get("fused"), "?")
     rl = roofline(kern_ms, local_bytes, K, config, world)
     rl["kernel"] = rl["kernel"].replace("k_query", path)
+    if world == 1:  # the clock this box ran the kernel at (a traced queue of 2 after the timing)
+        ts = trace_stats(eng, [ks[0] for _, ks in keyset[W:]], 2)
+        rl["shader_clock_ghz"] = ts["shader_clock_ghz"] if ts else None
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -662,7 +753,7 @@ def main():
             "value": round(shard_bytes / GIB / (m["ms1"] / 1e3), 3),
             "unit": "GiB/s",
             "note": "answer_dev per step (one launch per query, nothing queued behind it)",
-            "phases_ms": {k: r5(v) for k, v in m["phases1"].items() if k != "chunks"},
+            **single_phases(m["phases1"], m["ms1"]),
         },
         "inclusive_h2d_key_d2h_answer": {"ms_per_query": round(incl_ms, 4),
                                          "value": round(shard_bytes / GIB / (incl_ms / 1e3), 3),
@@ -721,13 +812,13 @@ def main():
         # the drop-in's setup -> first answer (north_star shape; configs[4]'s per-server shape)
         out["setup_c24"] = setup_leg(ctx, pir, 24, 1024, 1, 0)  # k = 1, r = 0: p = 2
         out["setup_c5"] = setup_leg(ctx, pir, 26, 1024, 5, 2, party=3)
-        out["configs1_c2"] = batch1_first(extra_leg(ctx, pir, "c2", W, K, rng))
+        out["configs1_c2"] = batch1_first(extra_leg(ctx, pir, "c2", W, K, rng, trace=8))
         if config != "c4":
             out["c4_single_engine"] = extra_leg(ctx, pir, "c4", min(W, 2), min(K, 16), rng,
                                                 single=False)
         if config != "c5":
             out["configs4_c5"] = extra_leg(ctx, pir, "c5", min(W, 3), min(K, 20), rng,
-                                           single=False)
+                                           single=False, trace=2)
         b = measure_batch(min(K, 8), min(W, 2), ctx, "c3b")
         out["configs2_c3b"] = {k: b[k] for k in ("value", "unit", "value_kind", "steps", "warmup",
                                                  "ms_per_step", "ms_per_key", "keys_per_s",
@@ -828,13 +919,15 @@ def exchange_fields(per_rank, world, host_fold, comm_err):
     return out
 
 
-def extra_leg(ctx, pir, config, W, K, rng, single=True):
-    """Another workload on this GPU (N = 1): queue and single-query rates."""
+def extra_leg(ctx, pir, config, W, K, rng, single=True, trace=0):
+    """Another workload on this GPU (N = 1): queue and single-query rates; trace > 0: one traced
+    queue of `trace` queries after the timed runs (shader clock, tile-0 head: trace_stats)."""
     n, efs, p, nq, _, workload = CONFIGS[config]
     keyset, fcw = make_keys(pir, n, p, nq, W + K, rng, ctx.local)
     eng = pir.Engine(p, 1, n, efs, nq, device=ctx.local)
     eng.fill_shard_random(SHARD_SEED)
     m = measure(ctx, eng, [ks[0] for _, ks in keyset], W, K, single=single)
+    tstats = trace_stats(eng, [ks[0] for _, ks in keyset[W:]], trace) if trace else None
     # every round's share property against parties 2 and p (all of them for p = 2)
     ok = pir_check(ctx, eng, keyset[W:W + 2], fcw, m["answers"], n, 0,
                    parties=sorted({2, p}))
@@ -849,10 +942,42 @@ def extra_leg(ctx, pir, config, W, K, rng, single=True):
            "k_query_ms_per_launch": r5(kern),
            "roofline_frac": round(gib * GIB * K / (kern / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if kern > 0 else None,
            "pir_record_recovered": ok}
+    if tstats:
+        res["trace"] = tstats
+    if config == "c5":  # compute-bound: the issue ports beside HBM
+        ck = tstats["shader_clock_ghz"]["median"] if tstats else None
+        iss = _pmc_issue(config, K, kern, ck)
+        res["roofline"] = {
+            "bound": "issue (scalar port: the four-Russians fold's index changes)",
+            "hbm_frac": res["roofline_frac"], "hbm_peak_GBps": HBM_PEAK_GBS,
+            **(iss or {"note": "profiles/pmc_c5.json is not stamped with this library"}),
+            "shader_clock_ghz": ck,
+            "note": "per plane of the fold: s_bfe_u32 + s_set_gpr_idx_idx (SALU) + 2 indexed "
+                    "v_xor (VALU); salu/valu_issue_frac = the launch's SALU / VALU instructions "
+                    "over the port capacity at this run's clock (1 SALU per CU-clock; 0.5 VALU "
+                    "per SIMD-clock x 4 SIMDs)"}
     if single:
         res["single_query"] = {"ms_per_query": r5(m["ms1"]),
                                "value": round(gib / (m["ms1"] / 1e3), 3), "unit": "GiB/s",
-                               "note": "batch = 1: one launch per query"}
+                               "note": "batch = 1: one launch per query",
+                               "k_query_ms": r5(m["phases1"].get("scan", float("nan"))),
+                               "k_reduce_ms": r5(m["phases1"].get("reduce", float("nan")))}
+        if config == "c2" and tstats:  # the lone query's floor model (Bounds)
+            head_ms = tstats["tile0_ready_us_median"] / 1e3
+            stream_ms = float(1 << n) * efs / (HBM_READ_MEASURED_GBS * 1e9) * 1e3
+            red_ms = m["phases1"].get("reduce", 0.0)
+            floor = head_ms + stream_ms + red_ms
+            res["single_query"]["roofline"] = {
+                "bound": "latency + stream: the dependent PRG head before the first row, then "
+                         "the shard at the measured read ceiling, then k_reduce",
+                "head_ms": r5(head_ms), "stream_ms": r5(stream_ms), "reduce_ms": r5(red_ms),
+                "floor_ms": r5(floor), "achieved_ms": r5(m["ms1"]),
+                "frac_of_floor": round(floor / m["ms1"], 4),
+                "hbm_frac": round(float(1 << n) * efs / (m["ms1"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "read_ceiling_GBps": HBM_READ_MEASURED_GBS,
+                "source": "head = median tile-0-ready stamp of this run's traced launch "
+                          "(key parse + 10-level descent + tile 0's 10 levels); stream = 1 GiB at "
+                          "profiles/r02_micro/read_bw.log's ceiling; reduce = this run's k_reduce"}
         res["queue_equals_one_at_a_time"] = bool(np.array_equal(m["answers"], m["singles"]))
     else:
         res["queue_equals_one_at_a_time"] = bool(q1)
@@ -929,7 +1054,10 @@ def batch1_first(res):
                     "roofline_frac": res.pop("roofline_frac"),
                     "note": "the same K queries answered as ONE queued launch"}
     res.update(ms_per_query=sq["ms_per_query"], value=sq["value"], unit="GiB/s",
-               value_kind="batch = 1: one launch per query (answer_dev), K queries back to back")
+               value_kind="batch = 1: one launch per query (answer_dev), K queries back to back",
+               k_query_ms=sq.get("k_query_ms"), k_reduce_ms=sq.get("k_reduce_ms"))
+    if "roofline" in sq:
+        res["roofline"] = sq["roofline"]
     return res
 
 
@@ -990,6 +1118,8 @@ def setup_leg(ctx, pir, L, f, k, r, party=1, T=16, check=True):
     q3 = time.perf_counter()
     sv.freeServer()
     q4 = time.perf_counter()
+    S.wait_freed()  # the teardown freeServer handed to the reaper thread (off the answer path)
+    q5 = time.perf_counter()
     cl.free_client()
     return {"workload": f"server setup -> first answer through pir_server.h: setSystemParams(L={L}, "
                         f"f={f}, k={k}, r={r}) -> p={p}, 2^{n} x {efs} B shard, NUM_ROUNDS={nq}; "
@@ -998,6 +1128,7 @@ def setup_leg(ctx, pir, L, f, k, r, party=1, T=16, check=True):
             "first_query_ms": round((q1 - q0) * 1e3, 4),
             "second_query_ms": round((q2 - q1) * 1e3, 4),
             "free_server_ms": round((q4 - q3) * 1e3, 4),
+            "free_server_background_teardown_ms": round((q5 - q4) * 1e3, 4),
             "client_files_gib": round((1 << L) * f / GIB, 3),
             "parity": parity,
             "note": "host wall clock; the setup encodes on the GPU from the client's host files "
@@ -1075,6 +1206,12 @@ def thread_leg(ctx, pir, eng, keys, want, shard_path, n, efs, T=16, K=10):
         whole = [sv.runOptimizedDPFTreeQuery(keys[q], 1) for q in range(K)]
         one_ms = (time.perf_counter() - t0) / K * 1e3
         ok_one = all(np.array_equal(whole[q], want[q]) for q in range(K))
+        # a lone Thread call (no partner within $PIR_SLICE_JOIN_US): the shim answers that
+        # slice alone, a 1/T pass; the fan-out's slice t of the same key is the check
+        sv.runOptimizedDPFTreeQueryThread(keys[0], 5, T)
+        t0 = time.perf_counter()
+        lone = [sv.runOptimizedDPFTreeQueryThread(keys[q], 5, T) for q in range(K)]
+        lone_ms = (time.perf_counter() - t0) / K * 1e3
     finally:
         sv.freeServer()
     # the round-3 shim: T per-slice engine answers one after another (each its own descent,
@@ -1086,6 +1223,7 @@ def thread_leg(ctx, pir, eng, keys, want, shard_path, n, efs, T=16, K=10):
            for q in range(Ks)]
     ser_ms = (time.perf_counter() - t0) / Ks * 1e3
     ok_ser = all(np.array_equal(ser[q], want[q]) for q in range(Ks))
+    ok_lone = all(np.array_equal(lone[q], eng.answer_slice(keys[q], 5, T)) for q in range(min(2, K)))
     gib = float(1 << n) * efs / GIB
     return {"workload": f"the reference call shape (tree.go:60-76) at the north_star shape: 2^{n} x {efs} B, "
                         f"p=2, T={T} concurrent runOptimizedDPFTreeQueryThread calls per query "
@@ -1096,16 +1234,21 @@ def thread_leg(ctx, pir, eng, keys, want, shard_path, n, efs, T=16, K=10):
             "ratio_vs_one_call": round(thr_ms / one_ms, 4),
             "python_threads_ms_per_query": r5(py_ms),
             "serialised_per_slice_ms_per_query": r5(ser_ms),
+            "lone_thread_call_ms": r5(lone_ms),
+            "lone_thread_call_over_one_call": round(lone_ms / one_ms, 4),
             "note": "host-buffer API through the pir_server.h shim (key upload, answer download, "
                     "sync); ms_per_query = T threads of pirRunTreeQueryThreads (C++ pool, the "
                     "goroutines of tree.go:60-76); python_threads = the same calls from T Python "
                     "threads through ctypes; one_call = runOptimizedDPFTreeQuery on the same "
                     "server; serialised_per_slice = T pir_engine_answer_slice calls in a row "
-                    "(the shim's round-3 behaviour)",
+                    "(the shim's round-3 behaviour); lone_thread_call = ONE "
+                    "runOptimizedDPFTreeQueryThread(t=5, T) with no partner call: the join wait "
+                    "($PIR_SLICE_JOIN_US, 200 us) + a 1/T pass",
             "parity": {"assembled_equals_device_answer": bool(ok),
                        "python_threads_assembled_equal": bool(ok_py),
                        "one_call_equals_device_answer": bool(ok_one),
-                       "serialised_slices_equal": bool(ok_ser)}}
+                       "serialised_slices_equal": bool(ok_ser),
+                       "lone_slice_equals_engine_slice": bool(ok_lone)}}
 
 
 def run_coefs(args, ctx, config):

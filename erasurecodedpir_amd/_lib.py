@@ -214,6 +214,7 @@ PROTOTYPES = {
                                       ctypes.c_void_p]),
     "pirServerSetRows": (None, [ctypes.POINTER(CServer), ctypes.c_void_p, ctypes.c_uint64,
                                 ctypes.c_uint64, ctypes.c_uint32]),
+    "pirServerWaitFreed": (None, []),
 }
 
 GLOBALS_INT = ["NUM_PARTIES", "NUM_FILES", "NUM_ENCODED_FILES", "LOG_NUM_ENCODED_FILES",

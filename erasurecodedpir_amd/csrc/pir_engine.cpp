@@ -330,7 +330,10 @@ int steal_args(pir_engine* e, const pir::QueryPlan& qp, int nk, int nslices, hip
   if (cap != hipStreamCaptureStatusNone) return PIR_OK;
   const size_t bytes = pir::query_steal_bytes(qp);
   if (bytes > e->steal_cap) {
-    if (e->d_steal) (void)hipFree(e->d_steal);
+    if (e->d_steal) {  // a launch still in flight may read the old buffer (as ensure_qcnt)
+      HIP_TRY(hipStreamSynchronize(s));
+      (void)hipFree(e->d_steal);
+    }
     e->d_steal = nullptr;
     e->steal_cap = 0;
     HIP_TRY(hipMalloc(&e->d_steal, bytes));
@@ -370,23 +373,17 @@ int answer_query(pir_engine* e, const pir::QueryPlan& qp, const uint8_t* d_raw, 
     HIP_TRY(hipMemsetAsync(d_out, 0, (size_t)nk * c.num_rounds * c.record_bytes, s));
   e->last_chunks = 1;
   e->last_fused = 2;
+  // profiling: k_query has no separate key / tree / scan kernels, so only its own bounds and
+  // the reduce are stamped (each event record between two launches costs the next one a few us
+  // of dispatch: fewer stamps keep the profiled answer close to the unprofiled one)
   hipEvent_t* ev = e->ev;
-  if (ev) {
-    HIP_TRY(hipEventRecord(ev[EV_KEY], s));
-    HIP_TRY(hipEventRecord(ev[EV_FRONT], s));
-    HIP_TRY(hipEventRecord(ev[EV_LEAF_B], s));
-    HIP_TRY(hipEventRecord(ev[EV_LEAF_E], s));
-    HIP_TRY(hipEventRecord(ev[EV_SCAN_B], s));
-  }
+  if (ev) HIP_TRY(hipEventRecord(ev[EV_SCAN_B], s));
   HIP_TRY(pir::launch_query(qp, d_raw, (uint32_t)e->key_len, nk, c.num_parties,
                             c.log_num_records, c.party_index - 1, log_parts_total, prefix,
                             e->d_shard + row0 * e->pitch, e->d_slabs, e->d_qscratch, s, nullptr,
                             fred ? d_out : nullptr, e->d_qcnt, c.record_bytes, (uint32_t)fred,
                             steal));
-  if (ev) {
-    HIP_TRY(hipEventRecord(ev[EV_SCAN_E], s));
-    HIP_TRY(hipEventRecord(ev[EV_PRERED], s));
-  }
+  if (ev) HIP_TRY(hipEventRecord(ev[EV_SCAN_E], s));
   if (!fred) HIP_TRY(pir::launch_reduce(sh, e->d_slabs, c.record_bytes, d_out, s, nk, nslices));
   if (ev) HIP_TRY(hipEventRecord(ev[EV_RED], s));
   return PIR_OK;
@@ -595,6 +592,12 @@ int ws_release(pir_engine* e, hipStream_t s, int rc) {
 const char* const kPhaseNames[] = {"key_prep", "tree_frontier", "tree_leaves", "scan",
                                    "reduce", "comm_fold", "total", "chunks", "fused"};
 constexpr int kNumPhases = 9;
+// the k_query path (fused == 2: key, tree and scan are one kernel): "launch" = answer start ->
+// k_query start (key upload, workspace ordering, dispatch), "scan" = the k_query launch,
+// "reduce" = k_reduce (0 with an in-kernel reduce), "comm_fold" = the split-shard exchange and
+// whatever follows; they add up to "total"
+const char* const kQueryPhaseNames[] = {"launch", "scan", "reduce", "comm_fold", "total", "fused"};
+constexpr int kNumQueryPhases = 6;
 
 // Mean per-phase device times over the answers recorded since the last read.  tree_leaves and
 // scan are the summed kernel durations of the C pipelined chunks (they overlap each other).
@@ -610,6 +613,24 @@ int read_timings(pir_engine* e, pir_kernel_time* out, int max) {
     sum += ms;
     return r;
   };
+  if (e->last_fused == 2) {
+    const int nq = std::min(max, kNumQueryPhases);
+    for (int k = 0; k < cnt; ++k) {
+      const hipEvent_t* v = e->prof[(e->prof_next + sz - cnt + k) % sz].ev;
+      HIP_TRY(el(v[EV_START], v[EV_SCAN_B], acc[0]));
+      HIP_TRY(el(v[EV_SCAN_B], v[EV_SCAN_E], acc[1]));
+      HIP_TRY(el(v[EV_SCAN_E], v[EV_RED], acc[2]));
+      HIP_TRY(el(v[EV_RED], v[EV_END], acc[3]));
+      HIP_TRY(el(v[EV_START], v[EV_END], acc[4]));
+    }
+    acc[5] = 2.0 * cnt;
+    for (int i = 0; i < nq; ++i) {
+      snprintf(out[i].name, sizeof out[i].name, "%s", kQueryPhaseNames[i]);
+      out[i].ms = (float)(acc[i] / cnt);
+    }
+    e->prof_count = 0;
+    return nq;
+  }
   for (int k = 0; k < cnt; ++k) {
     const hipEvent_t* v = e->prof[(e->prof_next + sz - cnt + k) % sz].ev;
     HIP_TRY(el(v[EV_START], v[EV_KEY], acc[0]));
@@ -1231,9 +1252,12 @@ int staged_h2d(pir_engine* e, uint64_t nchunks, size_t chunk_bytes, const Fill& 
   return rc;
 }
 
-// rows per staging chunk: ~64 MiB of `bytes_per_row`
+// rows per staging chunk: ~64 MiB of `bytes_per_row` ($PIR_STAGE_CHUNK_BYTES: tests use small
+// chunks so a small shard crosses several, with a ragged last one)
 uint64_t chunk_rows_for(uint64_t bytes_per_row) {
-  return std::max<uint64_t>(1, (64ull << 20) / std::max<uint64_t>(1, bytes_per_row));
+  uint64_t chunk = 64ull << 20;
+  if (const char* v = getenv("PIR_STAGE_CHUNK_BYTES")) chunk = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
+  return std::max<uint64_t>(1, chunk / std::max<uint64_t>(1, bytes_per_row));
 }
 
 }  // namespace
@@ -1557,9 +1581,11 @@ int pir_engine_reserve_queue(pir_engine_t* e, int num_keys) {
   int rc = ensure_slabs(e, (size_t)num_keys * pir::query_slab_bytes(qp));
   if (!rc) rc = ensure_buf(&e->d_qscratch, &e->qscratch_cap, pir::query_scratch_bytes(qp));
   if (!rc && e->fused_reduce) rc = ensure_qcnt(e, num_keys * 8, e->stream);
-  if (!rc && num_keys == 1) {  // the stealing buffer (the generation is not advanced here)
+  if (!rc && num_keys == 1) {  // the stealing buffer (this advances the generation once: harmless)
     pir::StealArgs st;
     rc = steal_args(e, qp, 1, 1, e->stream, &st);
+    // its zeroing ran on the engine stream: done before an answer on any other stream reads it
+    if (!rc) HIP_TRY(hipStreamSynchronize(e->stream));
   }
   if (!rc && e->comm) {
     const size_t total = (size_t)num_keys * c.num_rounds * c.record_bytes;

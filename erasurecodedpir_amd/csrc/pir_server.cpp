@@ -10,6 +10,7 @@
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/random.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -87,6 +88,7 @@ struct SliceGroup {
   std::vector<uint8_t> parts;     // num_threads x NUM_ROUNDS x efs (immutable once published)
   std::vector<uint8_t> taken;     // per slice, under ShimState::mu
   std::atomic<int> left{0};       // slices not yet copied out
+  std::atomic<int> joined{1};     // calls that found this group (the creator included)
   std::atomic<int> state{0};
   std::mutex m;
   std::condition_variable cv;
@@ -139,6 +141,22 @@ void sync_rows_down(server* s, ShimState* st) {
   st->host_stale = false;
 }
 
+// Whether any page of the row block is resident: initializeServer's rows are an untouched
+// anonymous mapping, so a resident page means something wrote (or read) indexList since.  A
+// setup then keeps the reference's host XOR-encode into those rows (client.cpp:88).
+bool rows_touched(const ShimState* st) {
+  const size_t bytes = (size_t)st->rows_alloc * st->row_bytes;
+  if (!st->row_block || !bytes) return false;
+  const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
+  std::vector<unsigned char> vec((bytes + pg - 1) / pg);
+  if (mincore(st->row_block, bytes, vec.data()) != 0) return true;  // cannot tell: assume data
+  for (unsigned char v : vec)
+    if (v & 1) return true;
+  return false;
+}
+
+void reaper_wait_idle();  // freeServer's deferred teardown (below): done before a new engine
+
 // Make sure the engine matches the current globals / nq and holds the current indexList
 // (upload = false: the caller is about to write the whole device shard itself).
 // must = false: return nullptr instead of aborting when no engine can be created (a setup on a
@@ -166,6 +184,7 @@ pir_engine_t* engine_for(server* s, ShimState* st, int nq, bool upload = true, b
     if (upload) sync_rows_down(s, st);  // the old engine holds the only copy of the shard
     if (st->eng) pir_engine_destroy(st->eng);
     st->eng = nullptr;
+    reaper_wait_idle();  // a freed server's device memory is released before this allocation
     if (pir_engine_create(&c, &st->eng) != PIR_OK) {
       if (must) die("pir_engine_create");
       st->eng = nullptr;
@@ -320,6 +339,66 @@ FanoutPool& fanout_pool() {
   static FanoutPool pool;
   return pool;
 }
+
+// freeServer's slow half off the caller's path.  The reference's RunTreeQuery calls FreeServer
+// BEFORE it stamps SendTime and returns the response (src/server_util/tree.go:90-100), so every
+// answer left behind the engine teardown (hipFree of the shard: 0.6-0.8 s at 16-64 GiB) and the
+// row block's munmap.  freeServer now detaches them and one reaper thread releases them; a new
+// engine (engine_for) waits until the reaper is idle, so device memory is back before it is
+// allocated again.  The destructor drains the queue at process exit.
+class Reaper {
+ public:
+  ~Reaper() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+  }
+  void post(std::function<void()> job) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      jobs_.push_back(std::move(job));
+      ++pending_;
+      if (!th_.joinable()) th_ = std::thread([this] { loop(); });
+    }
+    cv_.notify_all();
+  }
+  // returns once every job posted before the call has run
+  void wait_idle() {
+    std::unique_lock<std::mutex> lk(mu_);
+    idle_.wait(lk, [this] { return pending_ == 0; });
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [this] { return quit_ || !jobs_.empty(); });
+      if (jobs_.empty()) return;  // quit_ with nothing left
+      std::function<void()> job = std::move(jobs_.front());
+      jobs_.erase(jobs_.begin());
+      lk.unlock();
+      job();
+      lk.lock();
+      if (--pending_ == 0) idle_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, idle_;
+  std::vector<std::function<void()>> jobs_;
+  int pending_ = 0;
+  bool quit_ = false;
+  std::thread th_;
+};
+
+Reaper& reaper() {
+  static Reaper r;
+  return r;
+}
+
+void reaper_wait_idle() { reaper().wait_idle(); }
 
 int ceil_log2(long v) {
   int l = 0;
@@ -787,24 +866,42 @@ void initializeServer(server* s, int partyIndex, uint32_t logNumFiles, uint32_t 
 
 // server.cpp:45-52
 // No Thread call may start once freeServer has begun (the reference frees the rows under any
-// caller alike); one still inside its slice-group pass is waited for (the life lock).
+// caller alike); one still inside its slice-group pass is waited for (the life lock).  The
+// engine teardown and the row block's unmap run on the reaper thread (see Reaper): the call
+// returns once nothing can reach them any more, and the next engine created waits for them.
 void freeServer(server* s) {
   if (!s || !s->ctx) return;
   ShimState* st = static_cast<ShimState*>(s->ctx);
+  pir_engine_t* eng = nullptr;
   {
     std::lock_guard<std::mutex> lk(st->mu);
     std::unique_lock<std::shared_mutex> excl(st->life);
     st->groups.clear();
     st->group_bytes = 0;
-    if (st->eng) pir_engine_destroy(st->eng);
+    eng = st->eng;
     st->eng = nullptr;
   }
-  big_free(st->row_block);
-  free(s->indexList);
+  uint8_t* rows = st->row_block;
+  uint8_t** list = s->indexList;
   s->indexList = nullptr;
-  delete st;
   s->ctx = nullptr;
+  delete st;
+  if (getenv("PIR_SHIM_SYNC_FREE")) {  // the synchronous teardown (A/B timing)
+    if (eng) pir_engine_destroy(eng);
+    big_free(rows);
+    free(list);
+    return;
+  }
+  reaper().post([eng, rows, list] {
+    if (eng) pir_engine_destroy(eng);
+    big_free(rows);
+    free(list);
+  });
 }
+
+// Blocks until every freeServer teardown handed to the reaper has finished (tests, and callers
+// that measure device memory).
+void pirServerWaitFreed(void) { reaper_wait_idle(); }
 
 // server.cpp:96-134
 void runOptimizedDPFTreeQuery(server* s, uint8_t* key, int numQueries, uint8_t** result) {
@@ -817,15 +914,30 @@ void runOptimizedDPFTreeQuery(server* s, uint8_t* key, int numQueries, uint8_t**
   for (int a = 0; a < numQueries; ++a) memcpy(result[a], out.data() + a * efs, efs);
 }
 
+// How long the first Thread call of a query waits for a second call with the same key before it
+// answers its own slice alone ($PIR_SLICE_JOIN_US, default 200 us).  The T goroutines of
+// tree.go:60-76 start within microseconds of each other, so a fan-out still meets in one group
+// and pays one pass; a lone caller pays this wait plus a 1/T pass.
+int64_t slice_join_us() {
+  static const int64_t v = [] {
+    const char* s = getenv("PIR_SLICE_JOIN_US");
+    return s ? std::max<int64_t>(0, atoll(s)) : (int64_t)200;
+  }();
+  return v;
+}
+
 // server.cpp:505-549, intended semantics (see pir_server.h).  The T calls of one query
 // (tree.go:60-76: T goroutines, the same key) share ONE engine pass: the first to take the
-// server lock answers every slice (pir_engine_answer_slices), the rest copy theirs from it.
+// server lock opens a slice group and waits up to slice_join_us() for a partner; with one, it
+// answers every slice (pir_engine_answer_slices) and the rest copy theirs from it; without, it
+// closes the group and answers only its own slice (pir_engine_answer_slice: a 1/T pass).
 void runOptimizedDPFTreeQueryThread(server* s, uint8_t* key, int threadNum, int numThreads,
                                     uint8_t** result) {
   ShimState* st = state_of(s);
   std::shared_ptr<SliceGroup> g;
   pir_engine_t* e = nullptr;
   std::shared_lock<std::shared_mutex> pass;  // the computing call's hold on the engine
+  bool creator = false;
   const size_t efs = (size_t)ENCODED_FILE_SIZE_BYTES, ans = (size_t)NUM_ROUNDS * efs;
   {
     std::lock_guard<std::mutex> lk(st->mu);
@@ -850,9 +962,10 @@ void runOptimizedDPFTreeQueryThread(server* s, uint8_t* key, int threadNum, int 
       if (x->num_threads == numThreads && !x->taken[threadNum] &&
           memcmp(x->key.data(), key, klen) == 0) {
         g = x;
+        g->joined.fetch_add(1, std::memory_order_acq_rel);
         break;
       }
-    if (!g) {  // the first call of this query: it answers every slice
+    if (!g) {  // the first call of this query
       const size_t need = (size_t)numThreads * ans;
       while (!st->groups.empty() && (st->groups.size() >= kMaxSliceGroups ||
                                      st->group_bytes + need > kMaxSliceGroupBytes)) {
@@ -867,11 +980,39 @@ void runOptimizedDPFTreeQueryThread(server* s, uint8_t* key, int threadNum, int 
       g->taken.assign((size_t)numThreads, 0);
       g->left.store(numThreads, std::memory_order_relaxed);
       st->groups.push_back(g);
-      pass = std::shared_lock<std::shared_mutex>(st->life);  // no exclusive holder: we hold mu
+      creator = true;
     }
     g->taken[threadNum] = 1;
   }
-  if (pass.owns_lock()) {  // the one engine pass of the query, outside the server lock
+  if (creator) {  // wait (without the lock) for a partner, then decide under it
+    const int64_t wait_us = numThreads > 1 ? slice_join_us() : 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (g->joined.load(std::memory_order_acquire) < 2 &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(wait_us))
+      std::this_thread::yield();
+    bool solo;
+    {
+      std::lock_guard<std::mutex> lk(st->mu);
+      e = engine_for(s, st, NUM_ROUNDS);  // the engine may have been replaced meanwhile
+      solo = g->joined.load(std::memory_order_acquire) < 2;  // partners join under mu
+      if (solo) {  // close the group: later calls with this key open their own
+        auto it = std::find(st->groups.begin(), st->groups.end(), g);
+        if (it != st->groups.end()) {
+          st->group_bytes -= g->parts.size();
+          st->groups.erase(it);
+        }
+      }
+      pass = std::shared_lock<std::shared_mutex>(st->life);  // no exclusive holder: we hold mu
+    }
+    if (solo) {  // nobody else asked for this query: a 1/T pass for this slice alone
+      std::vector<uint8_t> out(ans);
+      const int rc = pir_engine_answer_slice(e, key, threadNum, numThreads, out.data());
+      pass.unlock();
+      if (rc != PIR_OK) die("runOptimizedDPFTreeQueryThread");
+      for (int a = 0; a < NUM_ROUNDS; ++a) memcpy(result[a], out.data() + a * efs, efs);
+      return;
+    }
+    // the one engine pass of the query, outside the server lock
     const int rc = pir_engine_answer_slices(e, key, numThreads, g->parts.data());
     pass.unlock();
     {
@@ -1121,6 +1262,12 @@ static bool gpu_setup(server* s, const std::function<int(pir_engine_t*)>& encode
   if (!s->ctx || getenv("PIR_SHIM_HOST_SETUP")) return false;
   ShimState* st = static_cast<ShimState*>(s->ctx);
   std::lock_guard<std::mutex> lk(st->mu);
+  // a caller may have written indexList directly (legal in the reference, which XORs the
+  // encoding into whatever the rows hold) without pirServerSetRows / pirServerShardChanged
+  if (st->rows_zero && rows_touched(st)) {
+    st->rows_zero = false;
+    st->dirty = true;
+  }
   if (!st->rows_zero) {  // rows already hold data: the host XOR-encode keeps that data
     std::unique_lock<std::shared_mutex> excl(st->life);
     sync_rows_down(s, st);
@@ -1131,6 +1278,11 @@ static bool gpu_setup(server* s, const std::function<int(pir_engine_t*)>& encode
     st->dirty = true;
     return false;
   }
+  // the encode rewrites the whole shard: no slice pass may read it meanwhile, and no slice
+  // group computed from the rows before the setup may be served after it
+  std::unique_lock<std::shared_mutex> excl(st->life);
+  st->groups.clear();
+  st->group_bytes = 0;
   if (encode(e) != PIR_OK) die("encode on the GPU");
   st->dirty = false;
   st->host_stale = true;

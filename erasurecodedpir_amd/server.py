@@ -156,8 +156,15 @@ class Server:
         return out
 
     def freeServer(self):
+        """Returns once the server is unreachable; the engine teardown runs in the background
+        (pirServerWaitFreed / wait_freed() waits for it)."""
         if self.s.ctx:
             self._lib.freeServer(ctypes.byref(self.s))
+
+
+def wait_freed():
+    """Block until every freeServer's background teardown has finished (pirServerWaitFreed)."""
+    _lib.load().pirServerWaitFreed()
 
     def __del__(self):
         try:

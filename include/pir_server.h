@@ -45,11 +45,27 @@
  * writes indexList directly after a setup calls pirServerSyncRows first ($PIR_SHIM_HOST_SETUP=1:
  * the reference's host encode into indexList, uploaded lazily on the first query).
  *
- * Cost model of runOptimizedDPFTreeQueryThread: the first of a query's T calls (same key, same T)
- * answers all T slices in ONE shard pass (pir_engine_answer_slices), the others copy their slice
- * out of it; a caller that issues slices of a query one at a time, or spreads them over servers,
- * pays a full pass per call.  At most 8 queries' slice groups (and 256 MiB of their parts) are
- * kept; the oldest is dropped first.
+ * Setup also stays on the host when indexList already holds data: rows written through
+ * pirServerSetRows / pirServerShardChanged, or written (or read) directly -- any resident page of
+ * the row block (mincore) -- so the encode is XORed into them as client.cpp:88 does.
+ *
+ * Cost model of runOptimizedDPFTreeQueryThread (N rows, T threads, one full pass = one shard
+ * read): the first of a query's calls (same key, same T) waits up to $PIR_SLICE_JOIN_US
+ * (default 200 us) for a second one.
+ *   - A partner arrives (the T goroutines of tree.go:60-76 start microseconds apart): the first
+ *     call answers all T slices in ONE full pass (pir_engine_answer_slices); the others copy
+ *     their slice out of it.  T calls cost one pass (+ the copies).
+ *   - No partner: the call answers its own slice alone (pir_engine_answer_slice: a descent to
+ *     node t and the scan of N/T rows), i.e. the wait + ~1/T of a pass + a lone query's head.
+ *     A caller that asks for slices one at a time, or spreads them over processes, pays that
+ *     per slice -- T slices then cost about one pass plus T heads and waits.
+ * At most 8 queries' slice groups (and 256 MiB of their parts) are kept; the oldest is dropped
+ * first.
+ *
+ * freeServer returns once no call can reach the server any more; the engine teardown (device
+ * memory) and the row block's unmap run on a background thread, and the next engine created
+ * (a setup or first query of any server) waits for them.  tree.go:90-100 frees the server
+ * BEFORE sending each answer, so this keeps the teardown off the response path.
  */
 #ifndef PIR_SERVER_H
 #define PIR_SERVER_H
@@ -249,6 +265,9 @@ void pirServerSyncRows(server *s);
  * -- what a test or benchmark would otherwise do row by row through indexList. */
 void pirServerSetRows(server *s, const uint8_t *rows, uint64_t row0, uint64_t nrows,
                       uint32_t rowBytes);
+/* Harness helper (no reference counterpart): block until every freeServer's background
+ * teardown has finished (device memory and host rows released). */
+void pirServerWaitFreed(void);
 
 #ifdef __cplusplus
 }

@@ -70,3 +70,71 @@ def test_rccl_self_check_fields():
     reh = bench.exchange_fields([_rank(r, w, attached=False, count=-1, user=-1) for r in range(w)],
                                 w, host_fold=True, comm_err=None)
     assert not reh["rccl_ranks_ok"] and reh["exchange"].endswith("(rehearsal)")
+
+
+class _FakeTraceEngine:
+    """trace_query's layout (include/pir_engine.h): wall stamps in us, shader-clock columns in
+    ticks / 100."""
+    key_len = 4
+
+    def __init__(self, ghz, nwg=8, tiles=6):
+        tr = np.zeros((nwg, 256))
+        tr[:, 0], tr[:, 2], tr[:, 3], tr[:, 6] = 0.0, 14.0, 43.0, 200.0
+        tr[:, 56], tr[:, 57] = 0.0, 14.0 * ghz * 1e3 / 100  # start -> first root
+        for g in range(tiles):
+            tr[:, 64 + g] = 43.0 + 35.0 * g
+            tr[:, 128 + g] = tr[:, 64 + g] * ghz * 1e3 / 100
+        self.tr = tr
+
+    def alloc_dev(self, n):
+        return 1
+
+    def free_dev(self, d):
+        pass
+
+    def h2d(self, d, b):
+        pass
+
+    def trace_query(self, d, nk):
+        return self.tr
+
+
+def test_leg_ceilings_and_clock_fields(monkeypatch, tmp_path):
+    """The per-leg ceilings the line carries: the shader clock from
+    k_query's stamps (trace_stats), configs[4]'s issue-port fractions from sha-stamped counters
+    (_pmc_issue, refused for another build), and the k_query phases that sum to the answer."""
+    import json
+    import bench
+    st = bench.trace_stats(_FakeTraceEngine(2.1), [b"k" * 4] * 4, 3)
+    assert abs(st["shader_clock_ghz"]["median"] - 2.1) < 1e-6
+    assert "tiles 0..5" in st["shader_clock_ghz"]["source"]
+    assert st["tile0_ready_us_median"] == 43.0
+    one = bench.trace_stats(_FakeTraceEngine(1.8, tiles=1), [b"k" * 4], 1)
+    assert abs(one["shader_clock_ghz"]["median"] - 1.8) < 1e-6 and "first tile root" in \
+        one["shader_clock_ghz"]["source"]
+    # counters: 2e9 SALU and 4e9 VALU per launch of 2 queries, stamped with the loaded library
+    root = tmp_path
+    (root / "profiles").mkdir()
+    d = {"lib_sha256": "abc", "queries_per_launch": 2,
+         "counters_per_launch": {"SQ_INSTS_SALU": 2e9, "SQ_INSTS_VALU": 4e9},
+         "issue": {"shader_clock_GHz_implied": 1.9}}
+    (root / "profiles" / "pmc_c5.json").write_text(json.dumps(d))
+    monkeypatch.setattr(bench, "ROOT", str(root))
+    monkeypatch.setattr(bench, "_lib_sha256", lambda: "abc")
+    iss = bench._pmc_issue("c5", 20, 70.0, 2.0)  # 20 queries in 70 ms at 2 GHz
+    cyc = 70e-3 * 2e9
+    assert abs(iss["salu_issue_frac"] - 2e10 / (256 * cyc)) < 1e-4
+    assert abs(iss["valu_issue_frac"] - 4e10 / (256 * 2 * cyc)) < 1e-4
+    assert iss["clock_source"] == "this run's k_query stamps"
+    assert bench._pmc_issue("c5", 20, 70.0, None)["clock_ghz_used"] == 1.9
+    monkeypatch.setattr(bench, "_lib_sha256", lambda: "other build")
+    assert bench._pmc_issue("c5", 20, 70.0, 2.0) is None
+    # k_query phases: launch + k_query + k_reduce + tail == the profiled answer
+    ph = {"launch": 0.004, "scan": 2.85, "reduce": 0.005, "comm_fold": 0.001, "total": 2.86,
+          "fused": 2.0}
+    sp = bench.single_phases(ph, 2.87)
+    assert set(sp["phases_ms"]) == {"launch", "k_query", "k_reduce", "exchange_and_tail"}
+    assert abs(sp["phases_sum_ms"] - 2.86) < 1e-9
+    assert abs(sp["phases_sum_over_ms_per_query"] - 2.86 / 2.87) < 1e-4
+    old = bench.single_phases({"key_prep": 0.1, "scan": 1.0, "chunks": 4, "fused": 0.0}, 1.2)
+    assert "chunks" not in old["phases_ms"] and "fused" not in old["phases_ms"]

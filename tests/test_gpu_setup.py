@@ -168,3 +168,97 @@ def test_engine_rows_roundtrip(S):
         bptrs = (ctypes.c_void_p * (1 << n))(*[back.ctypes.data + i * efs for i in range(1 << n)])
         _lib.check(lib.pir_engine_get_shard_rows(e._h, bptrs, 0, 1 << n), "get_shard_rows")
         assert np.array_equal(back, rows)
+
+
+def test_setup_free_setup_again(S):
+    """SETUP -> query -> freeServer -> SETUP -> query, three times (tree.go:90-100 frees the
+    server after every query): freeServer hands the engine teardown to the reaper thread and
+    returns at once; the next setup's engine waits for it; every answer is the oracle's."""
+    import time
+    import erasurecodedpir_amd as pir
+    L, f, k, r = 13, 256, 2, 1
+    p, n, nq, efs = _tree_setup(S, L, f, k, r)
+    cl = S.Client(L, f)
+    shard = O.encode_across(L, f, k, p, 2, O.synthetic_db(L, f))
+    keys = [pir.gen_keys(n, i * 311 + 5, p, nq, fcw=O.final_cw(p, nq, 1))[1] for i in range(3)]
+    frees = []
+    for i in range(3):
+        sv = S.Server(2, L, efs, 0, 4)
+        cl.encode_across_files_server(sv)
+        assert np.array_equal(sv.runOptimizedDPFTreeQuery(keys[i], nq),
+                              O.answer(p, 2, n, efs, nq, keys[i], shard)), i
+        assert np.array_equal(sv.runTreeQueryThreads(keys[i], 4),
+                              O.answer(p, 2, n, efs, nq, keys[i], shard)), i
+        t0 = time.perf_counter()
+        sv.freeServer()
+        frees.append(time.perf_counter() - t0)
+        assert not sv.s.ctx and not sv.s.indexList
+    S.wait_freed()
+    cl.free_client()
+    assert max(frees) < 0.05, frees  # the engine teardown is not on the caller's path
+
+
+def test_setup_over_directly_written_rows(S):
+    """indexList written directly (no pirServerSetRows / pirServerShardChanged) before the
+    setup: the encode is XORed INTO those rows as the reference does (client.cpp:88) -- the shim
+    sees the touched pages (mincore) and keeps the host encode; answers and rows are the
+    oracle's of (caller rows XOR encoding)."""
+    import erasurecodedpir_amd as pir
+    L, f, k, r = 12, 96, 2, 1
+    p, n, nq, efs = _tree_setup(S, L, f, k, r)
+    cl = S.Client(L, f)
+    enc = O.encode_across(L, f, k, p, 3, O.synthetic_db(L, f)).reshape(-1, efs)
+    mine = np.random.default_rng(8).integers(0, 256, enc.shape, dtype=np.uint8)
+    sv = S.Server(3, L, efs, 0, 4)
+    for i in range(1 << n):  # straight through the row pointers, as a C caller would
+        ctypes.memmove(sv.s.indexList[i], mine[i].ctypes.data, efs)
+    cl.encode_across_files_server(sv)
+    want = mine ^ enc
+    key = pir.gen_keys(n, 1234, p, nq, fcw=O.final_cw(p, nq, 1))[2]
+    assert np.array_equal(sv.runOptimizedDPFTreeQuery(key, nq),
+                          O.answer(p, 3, n, efs, nq, key, want.reshape(-1)))
+    assert np.array_equal(_rows(sv, n), want)
+    sv.freeServer()
+    cl.free_client()
+
+
+@pytest.mark.parametrize("chunk", [7 * 1000, 65536 + 40])
+def test_staging_many_chunks(S, monkeypatch, chunk):
+    """$PIR_STAGE_CHUNK_BYTES splits the staged copies into many small chunks with a ragged
+    last one: the double-buffer reuse (chunk c waits for c - 2's copy), get_shard_rows'
+    enqueue-ahead and encode_across_rows' per-chunk block mapping (blocks at j*n, file
+    encdb*j + row) are exercised; rows round-trip and both encodes equal the oracle's."""
+    import erasurecodedpir_amd as pir
+    from erasurecodedpir_amd import _lib
+    monkeypatch.setenv("PIR_STAGE_CHUNK_BYTES", str(chunk))
+    n, efs = 12, 200
+    with pir.Engine(2, 1, n, efs, 1) as e:
+        lib = _lib.load()
+        rows = np.random.default_rng(chunk).integers(0, 256, (1 << n, efs), dtype=np.uint8)
+        assert (1 << n) * efs // chunk >= 3  # several chunks
+        ptrs = (ctypes.c_void_p * (1 << n))(*[rows.ctypes.data + i * efs for i in range(1 << n)])
+        _lib.check(lib.pir_engine_set_shard_rows(e._h, ptrs, 0, 1 << n), "set_shard_rows")
+        assert np.array_equal(e.get_shard(0, 1 << n).reshape(-1, efs), rows)
+        back = np.zeros_like(rows)
+        bptrs = (ctypes.c_void_p * (1 << n))(*[back.ctypes.data + i * efs for i in range(1 << n)])
+        _lib.check(lib.pir_engine_get_shard_rows(e._h, bptrs, 0, 1 << n), "get_shard_rows")
+        assert np.array_equal(back, rows)
+    # encode across (k = 5: the last block past NUM_FILES is zero) and within, shim setups
+    L, f, k, r = 12, 100, 5, 2
+    p, n, nq, efs = _tree_setup(S, L, f, k, r)
+    cl = S.Client(L, f)
+    for party in (1, p):
+        sv = S.Server(party, L, efs)
+        cl.encode_across_files_server(sv)
+        assert np.array_equal(_rows(sv, n).reshape(-1),
+                              O.encode_across(L, f, k, p, party, O.synthetic_db(L, f))), party
+        sv.freeServer()
+    cl.free_client()
+    case = O.golden("hollanti.json")["cases"][0]
+    S.setSystemParams(case["L"], case["f"], case["t"], case["k"], case["r"], 0, case["rho"], 0, 3)
+    cl = S.Client(case["L"], case["f"])
+    sv = S.Server(1, case["L"], case["efs"])
+    cl.encode_within_files_server(sv)
+    assert O.sha(_rows(sv, case["L"])) == case["shard_sha256"][0]
+    sv.freeServer()
+    cl.free_client()

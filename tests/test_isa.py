@@ -95,3 +95,52 @@ def test_column_aes_rounds_issue_one_lookup_group():
     assert len(groups) > 100, "no column-shape AES rounds found in k_query"
     bad = [(f, n) for f, n in groups if n != 8]
     assert not bad, f"{len(bad)} of {len(groups)} rounds split: {bad[:5]}"
+
+
+def _fused_reduce_handoffs(asm):
+    """Per k_query instance with the in-kernel slab reduce (pir_kernels.hip, `if (out)`): the
+    returning counter add (global_atomic_add ... sc0) and what precedes / follows it."""
+    import re
+    out = []
+    fn, body = None, []
+
+    def flush():
+        if fn and "k_query" in fn:
+            ins = [ln.split("//")[0].strip() for ln in body]
+            for i, s in enumerate(ins):
+                if s.startswith("global_atomic_add ") and " sc0" in s:
+                    before = ins[:i]
+                    sc1 = any(t.startswith("global_store_dword") and " sc1" in t for t in before)
+                    # the last vector store of any kind (the non-fused branch's plain slab store
+                    # is laid out after the sc1 one) must be waited for before the add
+                    vst = [j for j, t in enumerate(before)
+                           if t.startswith(("global_store", "buffer_store", "flat_store", "scratch_store"))]
+                    between = before[vst[-1] + 1:] if vst else []
+                    waited = any(t.startswith("s_waitcnt") and "vmcnt(0)" in t for t in between)
+                    reloads = any(t.startswith("global_load_dword") and " sc1" in t for t in ins[i + 1:])
+                    out.append((fn, sc1, waited, reloads))
+    for ln in asm.split("\n"):
+        m = re.match(r"[0-9a-f]{16} <(\S+)>:", ln)
+        if m:
+            flush()
+            fn, body = m.group(1), []
+        elif fn:
+            body.append(ln)
+    flush()
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libpir_engine.so not built")
+def test_fused_reduce_handoff_is_write_through():
+    """The in-kernel slab reduce ($PIR_FUSED_REDUCE, off by default) hands the slabs to the last
+    workgroup WITHOUT release / acquire fences (round 5: each was an XCD-wide L2 write-back or
+    invalidate).  What makes it correct is gfx950-specific and is pinned here on the built
+    library: every k_query instance's slab stores are write-through (sc1), an s_waitcnt vmcnt(0)
+    separates the last vector store from the counter's returning atomic add, and the last
+    workgroup's slab reloads bypass the non-coherent caches (sc1).  A
+    compiler or ISA change that breaks this fails here instead of silently."""
+    import check_plane_asm as C
+    hs = _fused_reduce_handoffs(C.disassemble(LIB))
+    assert len(hs) >= 8, f"only {len(hs)} fused-reduce hand-offs found in k_query"
+    bad = [h for h in hs if not all(h[1:])]
+    assert not bad, bad[:4]

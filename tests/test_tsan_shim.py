@@ -30,7 +30,8 @@ def test_shim_threads_clean_under_tsan(tmp_path):
     if not shutil.which("g++") or not _have_tsan(tmp_path):
         pytest.skip("no g++ with ThreadSanitizer here")
     subprocess.check_call(["make", "-s", "-C", TSAN], stdout=subprocess.DEVNULL)
-    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66 second_deadlock_stack=1")
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66 second_deadlock_stack=1",
+               PIR_SLICE_JOIN_US="20000")  # fan-outs meet in one group under TSan's slow thread starts
     r = subprocess.run([os.path.join(TSAN, "build", "shim_threads")], capture_output=True,
                        text=True, env=env, timeout=600)
     assert "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]

@@ -9,10 +9,15 @@
 //   5. two pirRunTreeQueryThreads fan-outs at once (the shim's pool)
 //   6. a GPU-path setup (encode_across_files_server -> the engine; lazy host rows) with queries
 //      and pirServerSyncRows concurrently, then freeServer
+//   7. freeServer -> initializeServer + setup + queries while the reaper thread still tears the
+//      previous engine down (3 rounds), another server answering fan-outs throughout
+//   8. indexList written directly before the setup: the encode XORs into those rows
+//   9. lone Thread calls (no partner: the 1/T slice path), alone and beside a fan-out
 // Exit status 0 when every answer equals the oracle's (or, for 3, one of the two shards').
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
 #include <random>
 #include <thread>
 #include <vector>
@@ -198,6 +203,85 @@ int main() {
       rows_ok &= memcmp(s6.indexList[r], &want[r * efs6], efs6) == 0;
     CHECK(rows_ok, "scenario 6 rows after pirServerSyncRows");
     freeServer(&s6);
+
+    // 7. freeServer hands the engine to the reaper thread (the stub's teardown takes 20 ms):
+    //    set the next server up and query it while the previous teardown still runs, 3 times,
+    //    with a second server answering fan-outs throughout
+    server keep{};
+    initializeServer(&keep, 2, L6, f6, 0, 4);
+    encode_across_files_server(&c, &keep);
+    std::atomic<bool> stop{false};
+    std::atomic<int> keep_bad{0};
+    std::thread busy([&] {
+      std::vector<uint8_t> a(ans6);
+      uint8_t* ra[8];
+      for (int i = 0; i < nq6; ++i) ra[i] = a.data() + i * efs6;
+      const std::vector<uint8_t> want_a = oracle(k6k, 2, efs6, want);
+      while (!stop.load()) {
+        pirRunTreeQueryThreads(&keep, const_cast<uint8_t*>(k6k.party(2)), 4, ra);
+        if (a != want_a) keep_bad.fetch_add(1);
+      }
+    });
+    for (int it = 0; it < 3; ++it) {
+      server s7{};
+      initializeServer(&s7, 2, L6, f6, 0, T);
+      encode_across_files_server(&c, &s7);
+      std::vector<uint8_t> p7(T * ans6);
+      std::vector<std::thread> t7;
+      for (int t = 0; t < T; ++t)
+        t7.emplace_back([&, t] { slice(&s7, k6k.party(2), t, T, nq6, efs6, &p7[t * ans6]); });
+      for (auto& x : t7) x.join();
+      CHECK(xor_parts(p7, T, ans6) == oracle(k6k, 2, efs6, want), "scenario 7 answer, round %d", it);
+      freeServer(&s7);  // returns before the teardown is done
+      CHECK(s7.ctx == nullptr && s7.indexList == nullptr, "scenario 7 server not cleared");
+    }
+    stop.store(true);
+    busy.join();
+    CHECK(keep_bad.load() == 0, "scenario 7: %d wrong answers on the other server", keep_bad.load());
+    freeServer(&keep);
+    pirServerWaitFreed();
+
+    // 8. indexList written directly (no pirServerSetRows / ShardChanged) before the setup: the
+    //    encode is XORed into those rows (client.cpp:88), not written over them
+    {
+      server s8{};
+      initializeServer(&s8, 2, L6, f6, 0, T);
+      std::vector<uint8_t> mine(((size_t)1 << n6) * efs6), want8(want);
+      orc_xorshift_fill(0x51EDull, mine.data(), mine.size());
+      for (size_t r = 0; r < ((size_t)1 << n6); ++r) {
+        memcpy(s8.indexList[r], &mine[r * efs6], efs6);
+        for (int b = 0; b < efs6; ++b) want8[r * efs6 + b] ^= mine[r * efs6 + b];
+      }
+      encode_across_files_server(&c, &s8);
+      std::vector<uint8_t> p8(T * ans6);
+      std::vector<std::thread> t8;
+      for (int t = 0; t < T; ++t)
+        t8.emplace_back([&, t] { slice(&s8, k6k.party(2), t, T, nq6, efs6, &p8[t * ans6]); });
+      for (auto& x : t8) x.join();
+      CHECK(xor_parts(p8, T, ans6) == oracle(k6k, 2, efs6, want8), "scenario 8 answer");
+      bool ok8 = true;
+      for (size_t r = 0; r < ((size_t)1 << n6); ++r)
+        ok8 &= memcmp(s8.indexList[r], &want8[r * efs6], efs6) == 0;
+      CHECK(ok8, "scenario 8 rows");
+
+      // 9. lone Thread calls (no partner within the join window): each answers its own slice,
+      //    also while another query's fan-out runs on the same server
+      std::vector<uint8_t> one(ans6), ref(ans6);
+      slice(&s8, k6k.party(2), 3, T, nq6, efs6, one.data());
+      orc_answer_slice(p6, 2, n6, efs6, nq6, k6k.party(2), want8.data(), 3, T, ref.data());
+      CHECK(one == ref, "scenario 9 lone slice");
+      Keys k9 = make_keys(p6, n6, nq6, 5, 9);
+      std::vector<uint8_t> p9(T * ans6), lone(ans6), lref(ans6);
+      std::vector<std::thread> t9;
+      for (int t = 0; t < T; ++t)
+        t9.emplace_back([&, t] { slice(&s8, k9.party(2), t, T, nq6, efs6, &p9[t * ans6]); });
+      t9.emplace_back([&] { slice(&s8, k6k.party(2), 6, 2 * T, nq6, efs6, lone.data()); });
+      for (auto& x : t9) x.join();
+      CHECK(xor_parts(p9, T, ans6) == oracle(k9, 2, efs6, want8), "scenario 9 fan-out beside");
+      orc_answer_slice(p6, 2, n6, efs6, nq6, k6k.party(2), want8.data(), 6, 2 * T, lref.data());
+      CHECK(lone == lref, "scenario 9 lone slice beside a fan-out");
+      freeServer(&s8);
+    }
     free_client(&c);
   }
 #endif

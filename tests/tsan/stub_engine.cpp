@@ -7,6 +7,7 @@
 // here; the modes the TSan scenarios do not reach refuse.
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <mutex>
@@ -39,7 +40,15 @@ int pir_engine_create(const pir_engine_config* c, pir_engine_t** out) {
   return PIR_OK;
 }
 
-void pir_engine_destroy(pir_engine_t* e) { delete e; }
+// the real teardown frees device memory for hundreds of ms: slow enough here that freeServer's
+// reaper thread is still at it when the scenarios set the next server up
+void pir_engine_destroy(pir_engine_t* e) {
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    usleep(20000);
+  }
+  delete e;
+}
 
 uint64_t pir_engine_num_rows(const pir_engine_t* e) { return e ? e->rows : 0; }
 
@@ -111,6 +120,15 @@ int pir_engine_answer_slices(pir_engine_t* e, const uint8_t* key, int num_thread
   for (int t = 0; t < num_threads; ++t)
     orc_answer_slice(c.num_parties, c.party_index, c.log_num_records, (int)c.record_bytes,
                      c.num_rounds, key, e->shard.data(), t, num_threads, results + t * ans);
+  return PIR_OK;
+}
+
+int pir_engine_answer_slice(pir_engine_t* e, const uint8_t* key, int thread_num, int num_threads,
+                            uint8_t* result) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  const auto& c = e->cfg;
+  orc_answer_slice(c.num_parties, c.party_index, c.log_num_records, (int)c.record_bytes,
+                   c.num_rounds, key, e->shard.data(), thread_num, num_threads, result);
   return PIR_OK;
 }
 
