@@ -812,7 +812,7 @@ def main():
         # the drop-in's setup -> first answer (north_star shape; configs[4]'s per-server shape)
         out["setup_c24"] = setup_leg(ctx, pir, 24, 1024, 1, 0)  # k = 1, r = 0: p = 2
         out["setup_c5"] = setup_leg(ctx, pir, 26, 1024, 5, 2, party=3)
-        out["configs1_c2"] = batch1_first(extra_leg(ctx, pir, "c2", W, K, rng, trace=8))
+        out["configs1_c2"] = batch1_first(extra_leg(ctx, pir, "c2", W, K, rng, trace=1))
         if config != "c4":
             out["c4_single_engine"] = extra_leg(ctx, pir, "c4", min(W, 2), min(K, 16), rng,
                                                 single=False)
@@ -950,7 +950,8 @@ def extra_leg(ctx, pir, config, W, K, rng, single=True, trace=0):
         res["roofline"] = {
             "bound": "issue (scalar port: the four-Russians fold's index changes)",
             "hbm_frac": res["roofline_frac"], "hbm_peak_GBps": HBM_PEAK_GBS,
-            **(iss or {"note": "profiles/pmc_c5.json is not stamped with this library"}),
+            **(iss or {"counters": "profiles/pmc_c5.json is not stamped with this library: "
+                                   "no issue fractions quoted"}),
             "shader_clock_ghz": ck,
             "note": "per plane of the fold: s_bfe_u32 + s_set_gpr_idx_idx (SALU) + 2 indexed "
                     "v_xor (VALU); salu/valu_issue_frac = the launch's SALU / VALU instructions "

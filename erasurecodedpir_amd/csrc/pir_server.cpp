@@ -343,9 +343,11 @@ FanoutPool& fanout_pool() {
 // freeServer's slow half off the caller's path.  The reference's RunTreeQuery calls FreeServer
 // BEFORE it stamps SendTime and returns the response (src/server_util/tree.go:90-100), so every
 // answer left behind the engine teardown (hipFree of the shard: 0.6-0.8 s at 16-64 GiB) and the
-// row block's munmap.  freeServer now detaches them and one reaper thread releases them; a new
-// engine (engine_for) waits until the reaper is idle, so device memory is back before it is
-// allocated again.  The destructor drains the queue at process exit.
+// row block's munmap.  freeServer now detaches them and one reaper thread releases them, a few
+// ms later ($PIR_REAPER_DEFER_MS, default 20: unmapping tens of GiB holds the process's memory
+// map lock, which the caller's own page faults -- the response being sent -- would wait on); a
+// new engine (engine_for) waits until the reaper is idle (and has it start at once), so device
+// memory is back before it is allocated again.  The destructor drains the queue at exit.
 class Reaper {
  public:
   ~Reaper() {
@@ -359,36 +361,54 @@ class Reaper {
   void post(std::function<void()> job) {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      jobs_.push_back(std::move(job));
+      jobs_.push_back({std::move(job), std::chrono::system_clock::now() + defer()});
       ++pending_;
       if (!th_.joinable()) th_ = std::thread([this] { loop(); });
     }
     cv_.notify_all();
   }
-  // returns once every job posted before the call has run
+  // returns once every job posted before the call has run (they run now, not deferred)
   void wait_idle() {
     std::unique_lock<std::mutex> lk(mu_);
+    ++waiters_;
+    cv_.notify_all();
     idle_.wait(lk, [this] { return pending_ == 0; });
+    --waiters_;
   }
 
  private:
+  // (system_clock: libstdc++ waits on it with pthread_cond_timedwait, which ThreadSanitizer
+  // intercepts; a steady_clock wait_until becomes pthread_cond_clockwait, which gcc 11's does not)
+  struct Job {
+    std::function<void()> fn;
+    std::chrono::system_clock::time_point due;
+  };
+  static std::chrono::milliseconds defer() {
+    static const long ms = [] {
+      const char* v = getenv("PIR_REAPER_DEFER_MS");
+      return v ? std::max(0L, atol(v)) : 20L;
+    }();
+    return std::chrono::milliseconds(ms);
+  }
   void loop() {
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
       cv_.wait(lk, [this] { return quit_ || !jobs_.empty(); });
       if (jobs_.empty()) return;  // quit_ with nothing left
-      std::function<void()> job = std::move(jobs_.front());
+      const auto due = jobs_.front().due;
+      cv_.wait_until(lk, due, [this] { return quit_ || waiters_ > 0; });
+      Job job = std::move(jobs_.front());
       jobs_.erase(jobs_.begin());
       lk.unlock();
-      job();
+      job.fn();
       lk.lock();
       if (--pending_ == 0) idle_.notify_all();
     }
   }
   std::mutex mu_;
   std::condition_variable cv_, idle_;
-  std::vector<std::function<void()>> jobs_;
-  int pending_ = 0;
+  std::vector<Job> jobs_;
+  int pending_ = 0, waiters_ = 0;
   bool quit_ = false;
   std::thread th_;
 };
