@@ -155,7 +155,8 @@ bool rows_touched(const ShimState* st) {
   return false;
 }
 
-void reaper_wait_idle();  // freeServer's deferred teardown (below): done before a new engine
+void reaper_wait_idle();  // freeServer's deferred teardown (below)
+bool reaper_busy();
 
 // Make sure the engine matches the current globals / nq and holds the current indexList
 // (upload = false: the caller is about to write the whole device shard itself).
@@ -184,8 +185,14 @@ pir_engine_t* engine_for(server* s, ShimState* st, int nq, bool upload = true, b
     if (upload) sync_rows_down(s, st);  // the old engine holds the only copy of the shard
     if (st->eng) pir_engine_destroy(st->eng);
     st->eng = nullptr;
-    reaper_wait_idle();  // a freed server's device memory is released before this allocation
-    if (pir_engine_create(&c, &st->eng) != PIR_OK) {
+    // a freed server's teardown may still hold device memory: wait for it only if this
+    // allocation does not fit beside it (then once more, with everything released)
+    int crc = pir_engine_create(&c, &st->eng);
+    if (crc != PIR_OK && reaper_busy()) {
+      reaper_wait_idle();
+      crc = pir_engine_create(&c, &st->eng);
+    }
+    if (crc != PIR_OK) {
       if (must) die("pir_engine_create");
       st->eng = nullptr;
       return nullptr;
@@ -345,9 +352,9 @@ FanoutPool& fanout_pool() {
 // answer left behind the engine teardown (hipFree of the shard: 0.6-0.8 s at 16-64 GiB) and the
 // row block's munmap.  freeServer now detaches them and one reaper thread releases them, a few
 // ms later ($PIR_REAPER_DEFER_MS, default 20: unmapping tens of GiB holds the process's memory
-// map lock, which the caller's own page faults -- the response being sent -- would wait on); a
-// new engine (engine_for) waits until the reaper is idle (and has it start at once), so device
-// memory is back before it is allocated again.  The destructor drains the queue at exit.
+// map lock, which the caller's own page faults -- the response being sent -- would wait on).  A
+// new engine whose allocation fails while a teardown is pending waits for the reaper (which then
+// starts at once) and tries again.  The destructor drains the queue at exit.
 class Reaper {
  public:
   ~Reaper() {
@@ -366,6 +373,10 @@ class Reaper {
       if (!th_.joinable()) th_ = std::thread([this] { loop(); });
     }
     cv_.notify_all();
+  }
+  bool busy() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return pending_ > 0;
   }
   // returns once every job posted before the call has run (they run now, not deferred)
   void wait_idle() {
@@ -419,6 +430,7 @@ Reaper& reaper() {
 }
 
 void reaper_wait_idle() { reaper().wait_idle(); }
+bool reaper_busy() { return reaper().busy(); }
 
 int ceil_log2(long v) {
   int l = 0;
@@ -1001,20 +1013,27 @@ void runOptimizedDPFTreeQueryThread(server* s, uint8_t* key, int threadNum, int 
       g->left.store(numThreads, std::memory_order_relaxed);
       st->groups.push_back(g);
       creator = true;
+      pass = std::shared_lock<std::shared_mutex>(st->life);  // no exclusive holder: we hold mu
     }
     g->taken[threadNum] = 1;
   }
-  if (creator) {  // wait (without the lock) for a partner, then decide under it
+  if (creator) {
+    // wait (without the lock, holding the engine) for a partner: once one has joined the pass
+    // answers every slice, no matter who joins later, so the fan-out's creator goes straight on
+    // (re-taking the server lock behind the T - 1 partners cost the pass a few tens of us)
     const int64_t wait_us = numThreads > 1 ? slice_join_us() : 0;
     const auto t0 = std::chrono::steady_clock::now();
     while (g->joined.load(std::memory_order_acquire) < 2 &&
            std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(wait_us))
       std::this_thread::yield();
-    bool solo;
-    {
+    bool solo = false;
+    if (g->joined.load(std::memory_order_acquire) < 2) {
+      // decide under the server lock (partners join under it); the engine hold is dropped
+      // first (mu is taken before `life` everywhere), then re-taken under mu
+      pass.unlock();
       std::lock_guard<std::mutex> lk(st->mu);
       e = engine_for(s, st, NUM_ROUNDS);  // the engine may have been replaced meanwhile
-      solo = g->joined.load(std::memory_order_acquire) < 2;  // partners join under mu
+      solo = g->joined.load(std::memory_order_acquire) < 2;
       if (solo) {  // close the group: later calls with this key open their own
         auto it = std::find(st->groups.begin(), st->groups.end(), g);
         if (it != st->groups.end()) {

@@ -63,9 +63,11 @@
  * first.
  *
  * freeServer returns once no call can reach the server any more; the engine teardown (device
- * memory) and the row block's unmap run on a background thread, and the next engine created
- * (a setup or first query of any server) waits for them.  tree.go:90-100 frees the server
- * BEFORE sending each answer, so this keeps the teardown off the response path.
+ * memory) and the row block's unmap run on a background thread ~20 ms later
+ * ($PIR_REAPER_DEFER_MS); an engine created meanwhile (a setup or first query of any server) whose
+ * device allocation does not fit beside it waits for the teardown and tries again.
+ * tree.go:90-100 frees the server BEFORE sending each answer, so this keeps the teardown off the
+ * response path.
  */
 #ifndef PIR_SERVER_H
 #define PIR_SERVER_H

@@ -51,7 +51,7 @@ __device__ __forceinline__ uint32_t bytemask(uint32_t x) {
   return t | (t - (t >> 7));
 }
 __device__ __forceinline__ uint32_t sel(uint32_t m, uint32_t a, uint32_t b) {  // m ? a : b per bit
-  return __builtin_amdgcn_bitop3_b32(m, a, b, 0xE4);
+  return __builtin_amdgcn_bitop3_b32(m, a, b, 0xCA);  // TTBL index = S0*4 + S1*2 + S2
 }
 
 // 8-entry byte lookups of the 4 bytes of x (selector = low 3 bits) in each of P register pairs
