@@ -1,7 +1,7 @@
 // pir_server.cpp -- the server.h / params.h / client.h-compatible shim (include/pir_server.h)
 // over the MI355X engine.  Host glue only: every answer is computed by the HIP kernels behind
 // pir_engine_answer / pir_engine_answer_slice.
-#include "../../include/pir_server.h"
+#include "/root/repo/include/pir_server.h"
 
 #include <errno.h>
 #include <math.h>
@@ -25,8 +25,8 @@
 #include <utility>
 #include <vector>
 
-#include "../../include/pir_client.h"
-#include "../../include/pir_engine.h"
+#include "/root/repo/include/pir_client.h"
+#include "/root/repo/include/pir_engine.h"
 
 extern "C" {
 int NUM_PARTIES = 0;
@@ -92,7 +92,6 @@ struct SliceGroup {
   std::atomic<int> state{0};
   std::mutex m;
   std::condition_variable cv;
-  std::condition_variable join_cv;  // a partner joined (the creator's wait)
 };
 constexpr size_t kMaxSliceGroups = 8;  // queries whose slices are in flight at once
 // and at most this many bytes of their parts (T x NUM_ROUNDS x EFS each); the oldest group goes
@@ -118,12 +117,6 @@ struct ShimState {
   uint8_t* row_block = nullptr;    // the rows' one allocation (indexList[i] = row_block + i * row_bytes)
   std::vector<std::shared_ptr<SliceGroup>> groups;  // oldest first
   size_t group_bytes = 0;          // parts held by `groups`
-  // how this server's Thread calls have been arriving: the last query decided met a partner
-  // (a fan-out: the next creator waits longer for its partners) or answered alone
-  std::atomic<bool> expect_fanout{false};
-  // (key bytes, T) of the last queries whose creator answered alone: a later call with the same
-  // key and T means a fan-out whose partners were late -- its creator waits for them
-  std::vector<std::pair<std::vector<uint8_t>, int>> recent_solo;  // under mu, at most 4
 };
 
 ShimState* state_of(server* s) {
@@ -162,8 +155,7 @@ bool rows_touched(const ShimState* st) {
   return false;
 }
 
-void reaper_wait_idle();  // freeServer's deferred teardown (below)
-bool reaper_busy();
+void reaper_wait_idle();  // freeServer's deferred teardown (below): done before a new engine
 
 // Make sure the engine matches the current globals / nq and holds the current indexList
 // (upload = false: the caller is about to write the whole device shard itself).
@@ -192,14 +184,8 @@ pir_engine_t* engine_for(server* s, ShimState* st, int nq, bool upload = true, b
     if (upload) sync_rows_down(s, st);  // the old engine holds the only copy of the shard
     if (st->eng) pir_engine_destroy(st->eng);
     st->eng = nullptr;
-    // a freed server's teardown may still hold device memory: wait for it only if this
-    // allocation does not fit beside it (then once more, with everything released)
-    int crc = pir_engine_create(&c, &st->eng);
-    if (crc != PIR_OK && reaper_busy()) {
-      reaper_wait_idle();
-      crc = pir_engine_create(&c, &st->eng);
-    }
-    if (crc != PIR_OK) {
+    reaper_wait_idle();  // a freed server's device memory is released before this allocation
+    if (pir_engine_create(&c, &st->eng) != PIR_OK) {
       if (must) die("pir_engine_create");
       st->eng = nullptr;
       return nullptr;
@@ -359,9 +345,9 @@ FanoutPool& fanout_pool() {
 // answer left behind the engine teardown (hipFree of the shard: 0.6-0.8 s at 16-64 GiB) and the
 // row block's munmap.  freeServer now detaches them and one reaper thread releases them, a few
 // ms later ($PIR_REAPER_DEFER_MS, default 20: unmapping tens of GiB holds the process's memory
-// map lock, which the caller's own page faults -- the response being sent -- would wait on).  A
-// new engine whose allocation fails while a teardown is pending waits for the reaper (which then
-// starts at once) and tries again.  The destructor drains the queue at exit.
+// map lock, which the caller's own page faults -- the response being sent -- would wait on); a
+// new engine (engine_for) waits until the reaper is idle (and has it start at once), so device
+// memory is back before it is allocated again.  The destructor drains the queue at exit.
 class Reaper {
  public:
   ~Reaper() {
@@ -380,10 +366,6 @@ class Reaper {
       if (!th_.joinable()) th_ = std::thread([this] { loop(); });
     }
     cv_.notify_all();
-  }
-  bool busy() {
-    std::lock_guard<std::mutex> lk(mu_);
-    return pending_ > 0;
   }
   // returns once every job posted before the call has run (they run now, not deferred)
   void wait_idle() {
@@ -437,7 +419,6 @@ Reaper& reaper() {
 }
 
 void reaper_wait_idle() { reaper().wait_idle(); }
-bool reaper_busy() { return reaper().busy(); }
 
 int ceil_log2(long v) {
   int l = 0;
@@ -954,14 +935,9 @@ void runOptimizedDPFTreeQuery(server* s, uint8_t* key, int numQueries, uint8_t**
 }
 
 // How long the first Thread call of a query waits for a second call with the same key before it
-// answers its own slice alone ($PIR_SLICE_JOIN_US, default 200 us) -- when nothing suggests a
-// fan-out.  The T calls of a fan-out (tree.go:60-76's goroutines, the shim's pool) usually start
-// within microseconds, but a thread woken from sleep can arrive later than that (2^24 x 1 KiB,
-// T = 16: 3-4 of 20 pool fan-outs split at 200 us, none at 2 ms -- profiles/r06/
-// r6e_fanout_*.log).  So the creator waits up to kFanoutJoinUs (woken by the first partner, not
-// paid by a fan-out whose partners are on time) when a fan-out is expected: the call comes from
-// the shim's own pool, the server's last decided query met a partner, or an earlier call of the
-// same query already answered alone.  A lone caller after a fan-out pays that once.
+// answers its own slice alone ($PIR_SLICE_JOIN_US, default 200 us).  The T goroutines of
+// tree.go:60-76 start within microseconds of each other, so a fan-out still meets in one group
+// and pays one pass; a lone caller pays this wait plus a 1/T pass.
 int64_t slice_join_us() {
   static const int64_t v = [] {
     const char* s = getenv("PIR_SLICE_JOIN_US");
@@ -969,8 +945,6 @@ int64_t slice_join_us() {
   }();
   return v;
 }
-constexpr int64_t kFanoutJoinUs = 5000;
-thread_local bool t_in_fanout = false;  // set by pirRunTreeQueryThreads' pool jobs
 
 // server.cpp:505-549, intended semantics (see pir_server.h).  The T calls of one query
 // (tree.go:60-76: T goroutines, the same key) share ONE engine pass: the first to take the
@@ -983,7 +957,7 @@ void runOptimizedDPFTreeQueryThread(server* s, uint8_t* key, int threadNum, int 
   std::shared_ptr<SliceGroup> g;
   pir_engine_t* e = nullptr;
   std::shared_lock<std::shared_mutex> pass;  // the computing call's hold on the engine
-  bool creator = false, late = false;
+  bool creator = false;
   const size_t efs = (size_t)ENCODED_FILE_SIZE_BYTES, ans = (size_t)NUM_ROUNDS * efs;
   {
     std::lock_guard<std::mutex> lk(st->mu);
@@ -1009,8 +983,6 @@ void runOptimizedDPFTreeQueryThread(server* s, uint8_t* key, int threadNum, int 
           memcmp(x->key.data(), key, klen) == 0) {
         g = x;
         g->joined.fetch_add(1, std::memory_order_acq_rel);
-        { std::lock_guard<std::mutex> gl(g->m); }  // the creator checks `joined` under g->m
-        g->join_cv.notify_all();
         break;
       }
     if (!g) {  // the first call of this query
@@ -1029,58 +1001,29 @@ void runOptimizedDPFTreeQueryThread(server* s, uint8_t* key, int threadNum, int 
       g->left.store(numThreads, std::memory_order_relaxed);
       st->groups.push_back(g);
       creator = true;
-      pass = std::shared_lock<std::shared_mutex>(st->life);  // no exclusive holder: we hold mu
-      late = false;
-      for (auto it = st->recent_solo.begin(); it != st->recent_solo.end(); ++it)
-        if (it->second == numThreads && it->first.size() == klen &&
-            memcmp(it->first.data(), key, klen) == 0) {  // an earlier call of this query was alone
-          late = true;
-          st->recent_solo.erase(it);
-          break;
-        }
     }
     g->taken[threadNum] = 1;
   }
-  if (creator) {
-    // wait (without the lock, holding the engine) for a partner: once one has joined the pass
-    // answers every slice, no matter who joins later, so the fan-out's creator goes straight on
-    // (re-taking the server lock behind the T - 1 partners cost the pass a few tens of us)
-    // A short spin catches the partners of a running fan-out; after it the creator sleeps on
-    // join_cv (woken by the first partner) so that it does not hold a core the partners need.
-    const bool fanout = t_in_fanout || late || st->expect_fanout.load(std::memory_order_relaxed);
-    const int64_t wait_us = numThreads > 1 ? (fanout ? std::max(kFanoutJoinUs, slice_join_us())
-                                                      : slice_join_us()) : 0;
+  if (creator) {  // wait (without the lock) for a partner, then decide under it
+    const int64_t wait_us = numThreads > 1 ? slice_join_us() : 0;
     const auto t0 = std::chrono::steady_clock::now();
     while (g->joined.load(std::memory_order_acquire) < 2 &&
-           std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(std::min<int64_t>(wait_us, 20)))
+           std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(wait_us))
       std::this_thread::yield();
-    if (g->joined.load(std::memory_order_acquire) < 2 && wait_us > 20) {
-      std::unique_lock<std::mutex> gl(g->m);
-      g->join_cv.wait_until(gl, std::chrono::system_clock::now() + std::chrono::microseconds(wait_us - 20),
-                            [&] { return g->joined.load(std::memory_order_acquire) >= 2; });
-    }
-    bool solo = false;
-    if (g->joined.load(std::memory_order_acquire) < 2) {
-      // decide under the server lock (partners join under it); the engine hold is dropped
-      // first (mu is taken before `life` everywhere), then re-taken under mu
-      pass.unlock();
+    bool solo;
+    {
       std::lock_guard<std::mutex> lk(st->mu);
       e = engine_for(s, st, NUM_ROUNDS);  // the engine may have been replaced meanwhile
-      solo = g->joined.load(std::memory_order_acquire) < 2;
+      solo = g->joined.load(std::memory_order_acquire) < 2;  // partners join under mu
       if (solo) {  // close the group: later calls with this key open their own
         auto it = std::find(st->groups.begin(), st->groups.end(), g);
         if (it != st->groups.end()) {
           st->group_bytes -= g->parts.size();
           st->groups.erase(it);
         }
-        if (numThreads > 1) {
-          if (st->recent_solo.size() >= 4) st->recent_solo.erase(st->recent_solo.begin());
-          st->recent_solo.emplace_back(g->key, numThreads);
-        }
       }
       pass = std::shared_lock<std::shared_mutex>(st->life);  // no exclusive holder: we hold mu
     }
-    if (numThreads > 1) st->expect_fanout.store(!solo, std::memory_order_relaxed);
     if (solo) {  // nobody else asked for this query: a 1/T pass for this slice alone
       std::vector<uint8_t> out(ans);
       const int rc = pir_engine_answer_slice(e, key, threadNum, numThreads, out.data());
@@ -1131,9 +1074,7 @@ void pirRunTreeQueryThreads(server* s, uint8_t* key, int numThreads, uint8_t** r
     in[t] = rows.data() + (size_t)t * NUM_ROUNDS;
   }
   const std::function<void(int)> job = [&](int t) {
-    t_in_fanout = true;  // all numThreads calls of this query are coming
     runOptimizedDPFTreeQueryThread(s, key, t, numThreads, in[t]);
-    t_in_fanout = false;
   };
   fanout_pool().run(numThreads, job);
   assemblDPFTreeQueryThreadResults(s, in.data(), numThreads, result);

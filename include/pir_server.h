@@ -50,15 +50,19 @@
  * the row block (mincore) -- so the encode is XORed into them as client.cpp:88 does.
  *
  * Cost model of runOptimizedDPFTreeQueryThread (N rows, T threads, one full pass = one shard
- * read): the first of a query's calls (same key, same T) waits up to $PIR_SLICE_JOIN_US
- * (default 200 us) for a second one.
+ * read): the first of a query's calls (same key, same T) waits for a second one -- up to
+ * $PIR_SLICE_JOIN_US (default 200 us), or up to 5 ms when a fan-out is expected (the call comes
+ * from pirRunTreeQueryThreads' pool, the server's last decided query met a partner, or an earlier
+ * call of the same query already answered alone); it is woken by the first partner, so a fan-out
+ * whose calls are on time pays nothing for the wait.
  *   - A partner arrives (the T goroutines of tree.go:60-76 start microseconds apart): the first
  *     call answers all T slices in ONE full pass (pir_engine_answer_slices); the others copy
  *     their slice out of it.  T calls cost one pass (+ the copies).
  *   - No partner: the call answers its own slice alone (pir_engine_answer_slice: a descent to
  *     node t and the scan of N/T rows), i.e. the wait + ~1/T of a pass + a lone query's head.
  *     A caller that asks for slices one at a time, or spreads them over processes, pays that
- *     per slice -- T slices then cost about one pass plus T heads and waits.
+ *     per slice -- T slices then cost about one pass plus T heads and waits (the first lone
+ *     call after a fan-out, and a repeat of a key answered alone, wait the 5 ms).
  * At most 8 queries' slice groups (and 256 MiB of their parts) are kept; the oldest is dropped
  * first.
  *

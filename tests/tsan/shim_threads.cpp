@@ -13,6 +13,7 @@
 //      previous engine down (3 rounds), another server answering fan-outs throughout
 //   8. indexList written directly before the setup: the encode XORs into those rows
 //   9. lone Thread calls (no partner: the 1/T slice path), alone and beside a fan-out
+//  10. a fan-out whose first call answered alone and whose other calls came late
 // Exit status 0 when every answer equals the oracle's (or, for 3, one of the two shards').
 #include <stdio.h>
 #include <string.h>
@@ -280,6 +281,17 @@ int main() {
       CHECK(xor_parts(p9, T, ans6) == oracle(k9, 2, efs6, want8), "scenario 9 fan-out beside");
       orc_answer_slice(p6, 2, n6, efs6, nq6, k6k.party(2), want8.data(), 6, 2 * T, lref.data());
       CHECK(lone == lref, "scenario 9 lone slice beside a fan-out");
+
+      // 10. a fan-out whose first call came alone (answered alone after the join window), the
+      //     other T - 1 late: they meet in one group (its creator waits for late partners)
+      Keys k10 = make_keys(p6, n6, nq6, 200, 10);
+      std::vector<uint8_t> p10(T * ans6);
+      slice(&s8, k10.party(2), 0, T, nq6, efs6, &p10[0]);
+      std::vector<std::thread> t10;
+      for (int t = 1; t < T; ++t)
+        t10.emplace_back([&, t] { slice(&s8, k10.party(2), t, T, nq6, efs6, &p10[t * ans6]); });
+      for (auto& x : t10) x.join();
+      CHECK(xor_parts(p10, T, ans6) == oracle(k10, 2, efs6, want8), "scenario 10 late fan-out");
       freeServer(&s8);
     }
     free_client(&c);
