@@ -948,7 +948,9 @@ def extra_leg(ctx, pir, config, W, K, rng, single=True, trace=0):
         ck = tstats["shader_clock_ghz"]["median"] if tstats else None
         iss = _pmc_issue(config, K, kern, ck)
         res["roofline"] = {
-            "bound": "issue (scalar port: the four-Russians fold's index changes)",
+            "bound": "issue: the four-Russians fold's own instruction stream (4 per plane per "
+                     "scan wave; neither the scalar nor the vector port saturates -- "
+                     "profiles/r06/r6b_fold_mix.txt)",
             "hbm_frac": res["roofline_frac"], "hbm_peak_GBps": HBM_PEAK_GBS,
             **(iss or {"counters": "profiles/pmc_c5.json is not stamped with this library: "
                                    "no issue fractions quoted"}),
