@@ -1217,6 +1217,7 @@ def thread_leg(ctx, pir, eng, keys, want, shard_path, n, efs, T=16, K=10):
         lone_ms = (time.perf_counter() - t0) / K * 1e3
     finally:
         sv.freeServer()
+        S.wait_freed()  # its teardown (host rows, device shard) done before the next leg starts
     # the round-3 shim: T per-slice engine answers one after another (each its own descent,
     # tile-0 latency, reduce and sync)
     Ks = min(3, K)
