@@ -27,6 +27,10 @@
 #include "pir_kernels.h"
 #include "pir_mp.h"
 
+#ifndef PIR_TRACE_TREE_TILES
+#define PIR_TRACE_TREE_TILES 0  // diagnostics build only (pir_kernels.hip)
+#endif
+
 namespace {
 
 thread_local std::string g_err;
@@ -1963,7 +1967,13 @@ int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, int num_keys, 
   std::vector<uint64_t> h((size_t)nwg * pir::kQueryTraceSlots);
   hipError_t err = hipMemsetAsync(d_tr, 0, bytes, e->stream);
   const char* dbg = getenv("PIR_TRACE_NOSCAN");  // diagnostics: scan waves skip their rows
-  const uint64_t flags = (dbg && dbg[0] == '1') ? 1u : 0u;
+  uint64_t flags = (dbg && dbg[0] == '1') ? 1u : 0u;
+#if PIR_TRACE_TREE_TILES
+  if (const char* tv = getenv("PIR_TRACE_TILES")) {  // "a,b": two queue tiles' tree phases
+    unsigned a = 0, b = 0;
+    if (sscanf(tv, "%u,%u", &a, &b) >= 1) flags |= ((uint64_t)(a & 0xffu) << 8) | ((uint64_t)(b & 0xffu) << 16);
+  }
+#endif
   if (err == hipSuccess)
     err = hipMemcpyAsync(d_tr + (size_t)nwg * pir::kQueryTraceSlots, &flags, sizeof flags,
                          hipMemcpyHostToDevice, e->stream);
@@ -1984,7 +1994,7 @@ int pir_engine_trace_query(pir_engine_t* e, const uint8_t* d_key, int num_keys, 
       const uint64_t v = h[(size_t)w * pir::kQueryTraceSlots + k];
       // shader-clock ticks and counts as they are
       const bool raw = k == 56 || k == 57 || k == 59 || k == 60 || k == 61 ||
-                       (k >= 128 && k < 160) || k >= 192;
+                       (k >= 128 && k < 160) || (k >= 192 && !(PIR_TRACE_TREE_TILES && k >= 208));
       out[(size_t)w * pir::kQueryTraceSlots + k] = raw ? v : (v ? v - t0 : 0);
     }
   return nwg;

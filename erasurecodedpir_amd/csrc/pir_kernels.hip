@@ -1238,6 +1238,11 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(
 #endif
 constexpr int kTreeIlp = PIR_TREE_ILP;
 constexpr int kQueryCwCap = 256;  // (levels x (p-1)) correction words staged in LDS
+#ifndef PIR_TRACE_TREE_TILES
+// diagnostics build only: wave 0 of the tree team stamps two chosen queue tiles' phases into
+// trace[224 + 16 t + k] (tiles from the trace flags' bits 8-15 and 16-23, 0 = off)
+#define PIR_TRACE_TREE_TILES 0
+#endif
 constexpr int kQueryKin = 6;      // a tile's input nodes sit 6 levels below its root (64 of them)
 
 template <int TILE, int NRP, int NQ, int VEC, int GYMAX, int RING>
@@ -1256,6 +1261,7 @@ struct QuerySmem {
   uint32_t stk_t[kMaxLevels + 1];
   uint32_t bar, sbar, ready, lastq;
   uint32_t consumed[RING];
+  uint32_t prog[8];  // tiles each scan wave has consumed (scan_even mode 2)
 };
 
 __device__ __forceinline__ void cw_lds(const uint4* scw, const uint32_t* tcw, int L, uint32_t t,
@@ -1386,6 +1392,14 @@ __global__ __launch_bounds__(NT) void k_query(
   // diagnostics only: trace[kQueryTraceSlots * gridDim.x] bit 0 = scan waves skip their rows
   // (wrong answers; isolates the tree's rate beside the scan)
   const bool trace_flags_noscan = trace && (trace[(uint64_t)kQueryTraceSlots * gridDim.x] & 1u);
+#if PIR_TRACE_TREE_TILES
+  uint32_t tr_tile[2] = {0u, 0u};
+  if (trace) {
+    const uint64_t f = trace[(uint64_t)kQueryTraceSlots * gridDim.x];
+    tr_tile[0] = (uint32_t)(f >> 8) & 0xffu;
+    tr_tile[1] = (uint32_t)(f >> 16) & 0xffu;
+  }
+#endif
   if (trace) trace += (uint64_t)blockIdx.x * kQueryTraceSlots;
   if (trace && threadIdx.x == 0) { trace[0] = wall_clock64(); trace[56] = clock64(); }
   constexpr int NWV = NT / 64;  // waves per workgroup
@@ -1404,10 +1418,13 @@ __global__ __launch_bounds__(NT) void k_query(
   if (threadIdx.x == 0) {
     sm.bar = 0; sm.sbar = 0; sm.ready = 0;
     for (int r = 0; r < RING; ++r) sm.consumed[r] = 0;
+    for (int r = 0; r < 8; ++r) sm.prog[r] = 0;
   }
   // atomic_red: the answers were zeroed by a memset the host enqueued before this launch (on
   // the same stream), so no workgroup waits on another's progress
   const uint32_t tree_prio = (red_mode >> 8) & 3u;  // launch_query: $PIR_QUERY_TREE_PRIO
+  const uint32_t scan_even = (red_mode >> 10) & 3u;  // launch_query: $PIR_QUERY_SCAN_EVEN
+  const bool tree_rot = (red_mode >> 12) & 1u;       // launch_query: $PIR_QUERY_TREE_ROT
   red_mode &= 0xffu;
   const bool atomic_red = out && red_mode == 2;
   const uint32_t red_groups = red_mode == 3 ? 8u : 1u;  // slab groups of the last-add reduce
@@ -1582,6 +1599,19 @@ __global__ __launch_bounds__(NT) void k_query(
   };
   auto tree_tile = [&](uint32_t g, int nt, uint32_t team) __attribute__((always_inline)) {
     const uint32_t i = g % ntiles;
+    // levels narrower than the team run on its first waves; with tree_rot the team's waves take
+    // turns tile by tile (whole-wave rotation: lane positions, and so q / role, are unchanged),
+    // so that each SIMD's tree wave carries the same share and its scan waves the same slowdown
+    const int tt = (tree_rot && team != (uint32_t)NWV)
+                       ? (int)((threadIdx.x + 64u * (g % team)) % (uint32_t)nt) : (int)threadIdx.x;
+#if PIR_TRACE_TREE_TILES
+    uint64_t* tts = nullptr;  // this tile's stamp slots, if traced
+    if (trace && tt == 0 && g && (g == tr_tile[0] || g == tr_tile[1])) tts = trace + 224 + (g == tr_tile[0] ? 0 : 16);
+    if (tts) tts[0] = wall_clock64();
+#define PIR_TTS(k) do { if (tts) tts[k] = wall_clock64(); } while (0)
+#else
+#define PIR_TTS(k) do {} while (0)
+#endif
     const uint8_t* raw = raw0 + (size_t)(g / ntiles) * key_stride;
     uint8_t* ring = sm.ring[g % RING];
     // the whole workgroup: hardware barrier (waiting waves sleep); the tree waves alone: LDS
@@ -1692,6 +1722,7 @@ __global__ __launch_bounds__(NT) void k_query(
         if (trace && g == 0 && tt == 0 && tl < 16) trace[40 + tl] = wall_clock64();
         if (trace && g == 1 && tt == 0 && tl < 16) trace[160 + tl] = wall_clock64();
         ++tl;
+        if (tl < 12) PIR_TTS(1 + tl);
       }
     };
     // ---- super-tile root (wave 0, column shape, depth-first) ------------------------------
@@ -1780,6 +1811,7 @@ __global__ __launch_bounds__(NT) void k_query(
         t0[u] = fr_t[base + u];
       }
       sync();
+      PIR_TTS(1);
       expand_span(Lt, kQueryKin, KT - 1);
     } else {
       expand_span(Lt, 0, KT - 1);
@@ -1900,7 +1932,9 @@ __global__ __launch_bounds__(NT) void k_query(
         }
       }
     }
+    PIR_TTS(14);
     sync();  // every share of tile g is in the ring
+#undef PIR_TTS
     if constexpr (kSteal) {
       if (steal_on && g + 1 == total) {
         // the last tile's shares and the chunk counter reset as agent-scope (write-through)
@@ -1934,6 +1968,9 @@ __global__ __launch_bounds__(NT) void k_query(
     else if (tree_prio == 1) __builtin_amdgcn_s_setprio(1);
     for (uint32_t g = 1; g < total; ++g) {
       // slot g % RING free: every scan wave has consumed tile g - RING (per-slot counts)
+#if PIR_TRACE_TREE_TILES
+      if (trace && tt == 0 && (g == tr_tile[0] || g == tr_tile[1])) trace[224 + (g == tr_tile[0] ? 0 : 16) + 15] = wall_clock64();
+#endif
       if (g >= (uint32_t)RING) lds_wait_geq_idle(&sm.consumed[g % RING], (g / RING) * SW);
       tree_tile(g, TW * 64, TW);
     }
@@ -2102,6 +2139,22 @@ __global__ __launch_bounds__(NT) void k_query(
       const uint32_t i = g % ntiles;
       const uint8_t* ring = sm.ring[g % RING];
       PIR_FS(6);  // the previous tile's bookkeeping, end-of-query fold and slab
+      // Equal-priority waves issue oldest first, so of a SIMD's two scan waves the older one
+      // runs ahead and the younger one falls tiles behind -- and the slowest scan wave holds
+      // the ring slot the tree needs next.  A wave that starts tile g while another scan wave
+      // has not finished tile g - 1 drops one priority level for this tile.
+      if (scan_even == 1 && g > 0) {
+        if (lds_load(&sm.consumed[(g - 1) % RING]) < ((g - 1) / RING + 1) * SW)
+          __builtin_amdgcn_s_setprio(PIR_SCAN_PRIO - 1);
+        else
+          __builtin_amdgcn_s_setprio(PIR_SCAN_PRIO);
+      } else if (scan_even == 2 && g > 0 && SW >= 2 && SW <= 8) {
+        // the other scan wave on this wave's SIMD (waves are dealt to SIMDs round robin)
+        if (lds_load(&sm.prog[sw ^ (uint32_t)(SW / 2)]) < g)
+          __builtin_amdgcn_s_setprio(PIR_SCAN_PRIO - 1);
+        else
+          __builtin_amdgcn_s_setprio(PIR_SCAN_PRIO);
+      }
       lds_wait_geq(&sm.ready, g + 1);
       PIR_FS(0);  // waiting for the tree (tile g's shares)
       if (!UNI && scan) {  // per-lane coefficients: batches of U rows of this tile
@@ -2246,6 +2299,11 @@ __global__ __launch_bounds__(NT) void k_query(
         }
       }
       lds_signal(&sm.consumed[g % RING]);
+      if (scan_even == 2 && lane == 0 && sw < 8) __hip_atomic_store(&sm.prog[sw], g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#if PIR_TRACE_TREE_TILES
+      // every scan wave's consumed stamp of the two traced tiles (slots 208 + 8 t + sw)
+      if (trace && lane == 0 && (g == tr_tile[0] || g == tr_tile[1])) trace[208 + (g == tr_tile[0] ? 0 : 8) + sw] = wall_clock64();
+#endif
       if (trace && sw == 0 && lane == 0 && g < 32) trace[96 + g] = wall_clock64();
       if (i == ntiles - 1) {  // end of a query: sum_k alpha^k Z_k into LDS, then the slab
         const uint32_t qy = g / ntiles;
@@ -2421,7 +2479,13 @@ hipError_t query_nq_mp(const QueryPlan& qp, const uint8_t* d_key, uint32_t key_s
   if (!sh.uniform) return hipErrorInvalidValue;
   // tree-wave priority as launch_query (a lone query's share waves at 3)
   const char* tp = getenv("PIR_QUERY_TREE_PRIO");
-  const uint32_t rm = ((tp ? (uint32_t)atoi(tp) : (nk == 1 ? 3u : 0u)) & 3u) << 8;
+  uint32_t rm = ((tp ? (uint32_t)atoi(tp) : (nk == 1 ? 3u : 0u)) & 3u) << 8;
+  {  // the four-Russians shape's 8 scan waves: evened and rotated as in launch_query
+    const char* se = getenv("PIR_QUERY_SCAN_EVEN");
+    rm |= ((se ? (uint32_t)atoi(se) : (qp.m4r ? 2u : 0u)) & 3u) << 10;
+    const char* tr = getenv("PIR_QUERY_TREE_ROT");
+    if (tr ? atoi(tr) != 0 : qp.m4r) rm |= 1u << 12;
+  }
   // mp_tile gives each of its threads at most ONE 16-record CTR block of the tile (no loop
   // over blocks): the share waves (TW * 64 threads; tile 0: all NTH) must cover TILE / 16 blocks
 #define PIR_QMP(TW, NTH)                                                                         \
@@ -2943,6 +3007,21 @@ hipError_t launch_query(const QueryPlan& qp, const uint8_t* d_raw, uint32_t key_
   {
     const char* tp = getenv("PIR_QUERY_TREE_PRIO");
     red_mode |= ((tp ? (uint32_t)atoi(tp) : ((nk == 1 || qp.m4r) ? 3u : 0u)) & 3u) << 8;
+    // Round 6: with 8 scan waves (two per SIMD), the older of a SIMD's two equal-priority scan
+    // waves ran 2-3 tiles ahead of the younger one and the younger one held the ring slot the
+    // tree needed next (configs[4] trace: the tree waited 11-15 us per tile for a slot).  The
+    // scan waves now yield to a lagging SIMD mate (mode 2; 1 = to any lagging wave), and the
+    // tree team's waves take turns at the levels narrower than the team (tree_rot), so every
+    // SIMD carries the same tree share: configs[4] queue 3.27-3.37 -> 3.16-3.23 ms, 3-4 round
+    // queues -3 %, configs[1] lone -1-2 %, the north_star queue -0.5 %; the 12-tree-wave shape
+    // of small records (4 scan waves, one per SIMD) lost 5 % and keeps both off
+    // (profiles/r06/r6p_c5_even_ab.log, r6q_*, r6s_shapes_ab.log).  $PIR_QUERY_SCAN_EVEN = 0-2
+    // and $PIR_QUERY_TREE_ROT = 0/1 override.
+    const bool even_def = qp.m4r || qp.tw == kFusedTW;
+    const char* se = getenv("PIR_QUERY_SCAN_EVEN");
+    red_mode |= ((se ? (uint32_t)atoi(se) : (even_def ? 2u : 0u)) & 3u) << 10;
+    const char* tr = getenv("PIR_QUERY_TREE_ROT");
+    if (tr ? atoi(tr) != 0 : even_def) red_mode |= 1u << 12;
   }
 #define PIR_Q(NQ, TL) query_nq<NQ, TL>(qp, d_raw, key_stride, nk, p, n, party0, log_parts, prefix, shard, slabs, scratch, s, trace, out, qcnt, efs, red_mode, steal)
 #ifdef PIR_DEV_NQ  // development builds only (ISA / register checks): one round count

@@ -80,6 +80,26 @@ def main():
             t1 = [med[176]] + [med[160 + k] for k in range(16) if tr[:, 160 + k].all()]
             print("  tile-1 root + level ends (med us, tree waves beside the scan):",
                   " ".join(f"{v:.1f}" for v in t1), f"| ready {med[65]:.1f}")
+            # diagnostics build (-DPIR_TRACE_TREE_TILES=1) with $PIR_TRACE_TILES=a,b: two queue
+            # tiles' tree phases (wave 0 of the tree team): slot wait, entry, inputs, levels, leaf, ready
+            tv = os.environ.get("PIR_TRACE_TILES")
+            if tv:
+                for t, g in enumerate(int(x) for x in tv.split(",")[:2]):
+                    base = 224 + 16 * t
+                    col = lambda k: tr[:, base + k]
+                    if not col(0).all():
+                        continue
+                    lev = [k for k in range(2, 14) if col(k).all()]
+                    parts = [("slot_wait", 15), ("entry", 0), ("inputs", 1)] + [(f"L{k - 1}", k) for k in lev] + [("leaf", 14)]
+                    print(f"  tree tile {g}: " + "  ".join(f"{n} {np.median(col(k)):.1f}" for n, k in parts)
+                          + f"  ready {med[64 + g]:.1f}  consumed[{g - 1}] {med[96 + g - 1]:.1f}  consumed[{g}] {med[96 + g]:.1f}")
+                    if tr[:, 208 + 8 * t:216 + 8 * t].all():
+                        sw = np.median(tr[:, 208 + 8 * t:216 + 8 * t], axis=0)
+                        blk = tr[:, 208 + 8 * t:216 + 8 * t]
+                        spread = blk.max(axis=1) - blk.min(axis=1)
+                        print(f"    scan waves' consumed[{g}] (med us, sw 0-7): " + " ".join(f"{v:.1f}" for v in sw)
+                              + f"  | per-workgroup spread med {np.median(spread):.1f} max {spread.max():.1f} us,"
+                              + f" slowest sw histogram {np.bincount(blk.argmax(axis=1), minlength=8).tolist()}")
     e.close()
 
 
