@@ -765,6 +765,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
 //   VEC <= 2, NQ >= 3 : the 8 plane masks from the table (s_load_dwordx8, one round ahead;
 //             per-bit s_bfe masks held the 8-round batched scan to 1.5 TB/s on the scalar unit).
 // Wave w folds rows [w * nrec / nwaves, (w + 1) * nrec / nwaves) of its column group.
+constexpr uint32_t kScanDynRows = 32;  // k_scan_uni's claimed chunks (four Russians, dyn)
 template <int NQ, int NRP, int VEC, int NT = kScanThreads>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kScanThreads ? kScanThreads / 64 * kScanBlocksPerCU / 4 : NT / 256)))
 void k_scan_uni(const uint8_t* __restrict__ shard,
@@ -781,7 +782,12 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
   constexpr bool kM4R = (VEC == 1 && NQ >= 4 && NQ <= 8 && NRP >= 4 && NRP <= 8) ||
                         (VEC == 2 && NQ >= 4 && NQ <= 5 && NT == kScanM4rThreads);
   constexpr bool kAsm = !kBranch && !kM4R && VEC <= 2 && NQ >= 3;
+  // accumulate bit 1 (launch_scan, $PIR_SCAN_DYN): the four-Russians waves claim chunks of the
+  // workgroup's rows instead of folding a fixed range each
+  const bool dyn = (kM4R ? PIR_M4R_SLOAD != 0 : NQ <= 5) && ((accumulate >> 1) & 1);
+  accumulate &= 1;
   __shared__ uint32_t red[NQ * GW];
+  __shared__ uint32_t next_chunk;
   for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) red[i] = 0;
 
   const uint32_t lane = threadIdx.x & 63;
@@ -800,7 +806,174 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
 #pragma unroll
       for (int v = 0; v < VEC; ++v) Z[a][k][v] = 0;
 
-  if (r1 > r0) {
+  // one row's fold into the planes: row j of the 64-row coefficient block c4 (lane l holds
+  // row l's coefficient bytes)
+  auto fold_j = [&](const Chunk<VEC>& xr, const uint4& c4, uint32_t j) __attribute__((always_inline)) {
+    const uint4 cf = make_uint4(__builtin_amdgcn_readlane(c4.x, j),
+                                NRP > 4 ? __builtin_amdgcn_readlane(c4.y, j) : 0u,
+                                NRP > 8 ? __builtin_amdgcn_readlane(c4.z, j) : 0u,
+                                NRP > 8 ? __builtin_amdgcn_readlane(c4.w, j) : 0u);
+    if constexpr (kAsm) {
+      u32x8 m = plane_masks_issue(coef_byte(cf, 0));
+#pragma unroll
+      for (int a = 0; a < NQ; ++a) {
+        if constexpr (VEC == 2) {
+          auto& Za = reinterpret_cast<uint32_t(&)[8][2]>(Z[a]);
+          if (a + 1 < NQ) m = planes_fold2_next(Za, xr.v[0], xr.v[1], m, coef_byte(cf, a + 1));
+          else planes_fold2(Za, xr.v[0], xr.v[1], m);
+        } else {
+          auto& Za = reinterpret_cast<uint32_t(&)[8][1]>(Z[a]);
+          if (a + 1 < NQ) m = planes_fold1_next(Za, xr.v[0], m, coef_byte(cf, a + 1));
+          else planes_fold1(Za, xr.v[0], m);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int a = 0; a < NQ; ++a) {
+        const uint32_t ca = coef_byte(cf, a);
+        if constexpr (kBranch) {
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk)
+            if (ca & (1u << kk)) {
+#pragma unroll
+              for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= xr.v[v];
+            }
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk) {
+            const uint32_t m = 0u - ((ca >> kk) & 1u);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) Z[a][kk][v] = mxor(Z[a][kk][v], xr.v[v], m);
+          }
+        }
+      }
+    }
+  };
+  if constexpr (!kM4R && NQ <= 5) {  // (6-8 rounds take k_scan_t; the wider instances spill)
+    if (dyn) {
+      // as the four-Russians chunks below, for the per-row folds: chunks of the 64-row
+      // coefficient block, the next chunk's coefficients and first rows in flight
+      constexpr uint32_t C = 64;
+      if (threadIdx.x == 0) next_chunk = 0;
+      __syncthreads();
+      const uint64_t wg0 = (uint64_t)blockIdx.x * waves_per_block;
+      const uint64_t R0 = rfl64(wg0 * nrec / nwaves);
+      const uint32_t nrows = (uint32_t)__builtin_amdgcn_readfirstlane(
+          (uint32_t)((wg0 + waves_per_block) * nrec / nwaves - wg0 * nrec / nwaves));
+      const uint32_t nch = (nrows + C - 1) / C;
+      const uint8_t* base = shard + (uint64_t)(active ? chunk : 0u) * CH + R0 * pitch;
+      auto claim = [&]() __attribute__((always_inline)) -> uint32_t {
+        uint32_t v = 0;
+        if (lane == 0)
+          v = __hip_atomic_fetch_add(&next_chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return (uint32_t)__builtin_amdgcn_readfirstlane(v);
+      };
+      auto rowp = [&](uint32_t ch, uint32_t k) __attribute__((always_inline)) -> uint32_t {
+        const uint32_t o = ch * C + k;
+        return ch < nch && o < nrows ? o : 0u;
+      };
+      auto coefs_ch = [&](uint32_t ch) __attribute__((always_inline)) {
+        const uint32_t o = ch * C + lane;
+        return ch < nch && o < nrows ? load_coef<NRP>(c, R0 + o) : make_uint4(0, 0, 0, 0);
+      };
+      uint32_t cur = claim();
+      if (cur < nch) {
+        uint32_t nxt = claim();
+        Chunk<VEC> x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = load_chunk<VEC>(base + (uint64_t)rowp(cur, u) * pitch);
+        uint4 c4 = coefs_ch(cur);
+        while (true) {
+          const uint4 c4n = coefs_ch(nxt);
+          const uint32_t nb = nrows - cur * C < C ? nrows - cur * C : C;
+          for (uint32_t j0 = 0; j0 < C; j0 += U) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const uint32_t j = j0 + u;
+              if (j < nb) fold_j(x[u], c4, j);  // wave-uniform
+              const uint32_t k = j + U;
+              x[u] = load_chunk<VEC>(base + (uint64_t)(k < C ? rowp(cur, k) : rowp(nxt, k - C)) * pitch);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+          cur = nxt;
+          c4 = c4n;
+          if (cur >= nch) break;
+          nxt = claim();
+        }
+      }
+    }
+  }
+#if PIR_M4R_SLOAD
+  if constexpr (kM4R) {
+    if (dyn) {
+      // Equal-priority waves issue oldest first, so with a fixed row range per wave the oldest
+      // waves of a SIMD finish first and the youngest ones fold the tail alone.  Here the
+      // workgroup's rows are chunks of kScanDynRows claimed one at a time (an LDS counter, the
+      // next chunk claimed while the current one folds, so the rolling row / coefficient loads
+      // run ahead across chunk boundaries); every wave's planes are XORed into red[] at the
+      // end, so which wave folds a chunk does not matter.  Rows past the workgroup's last take
+      // coefficient 0 and re-read its first row.
+      constexpr uint32_t C = kScanDynRows;
+      if (threadIdx.x == 0) next_chunk = 0;
+      __syncthreads();
+      const uint64_t wg0 = (uint64_t)blockIdx.x * waves_per_block;
+      const uint64_t R0 = rfl64(wg0 * nrec / nwaves);
+      const uint32_t nrows = (uint32_t)__builtin_amdgcn_readfirstlane(
+          (uint32_t)((wg0 + waves_per_block) * nrec / nwaves - wg0 * nrec / nwaves));
+      const uint32_t nch = (nrows + C - 1) / C;
+      using CW = std::conditional_t<NRP == 8, uint64_t, uint32_t>;
+      typedef const __attribute__((address_space(4))) CW* ConstCW;
+      const ConstCW cwb = (ConstCW)(const CW*)c + R0;
+      const uint8_t* base = shard + (uint64_t)(active ? chunk : 0u) * CH + R0 * pitch;
+      auto claim = [&]() __attribute__((always_inline)) -> uint32_t {
+        uint32_t v = 0;
+        if (lane == 0)
+          v = __hip_atomic_fetch_add(&next_chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return (uint32_t)__builtin_amdgcn_readfirstlane(v);
+      };
+      uint32_t cur = claim();
+      if (cur < nch) {
+        uint32_t nxt = claim();
+        Chunk<VEC> x[4];
+        uint64_t w[4];
+        bool wv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t o = cur * C + (uint32_t)r;
+          wv[r] = o < nrows;
+          w[r] = (uint64_t)cwb[wv[r] ? o : 0u];
+          x[r] = load_chunk<VEC>(base + (uint64_t)(wv[r] ? o : 0u) * pitch);
+        }
+        while (true) {
+          for (uint32_t i = 0; i < C; i += 4) {
+            const uint32_t vi = m4r_index(rfl64(wv[0] ? w[0] : 0), rfl64(wv[1] ? w[1] : 0),
+                                          rfl64(wv[2] ? w[2] : 0), rfl64(wv[3] ? w[3] : 0));
+            __builtin_amdgcn_sched_barrier(0);
+            // the next group: this chunk's, or the first of the next chunk
+            const uint32_t nc = i + 4 < C ? cur : nxt, ni = i + 4 < C ? i + 4 : 0u;
+            uint32_t o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              o[r] = nc * C + ni + (uint32_t)r;
+              wv[r] = nc < nch && o[r] < nrows;
+              if (!wv[r]) o[r] = 0u;
+              w[r] = (uint64_t)cwb[o[r]];
+            }
+            m4r_fold_group<VEC, NQ>(Z, x[0].v, x[1].v, x[2].v, x[3].v, vi, (lane & 7u) * 4u);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) x[r] = load_chunk<VEC>(base + (uint64_t)o[r] * pitch);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          cur = nxt;
+          if (cur >= nch) break;
+          nxt = claim();
+        }
+      }
+    }
+  }
+#endif
+  if (!dyn && r1 > r0) {
     // inactive lanes read the row's first chunk (their planes are never written out); slots past
     // the wave's last row re-read its first row (never folded)
     const uint8_t* base = shard + (uint64_t)(active ? chunk : 0u) * CH;
@@ -870,47 +1043,7 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const uint32_t j = j0 + u;
-          if (j < nb) {  // wave-uniform
-            const uint4 cf = make_uint4(__builtin_amdgcn_readlane(c4.x, j),
-                                        NRP > 4 ? __builtin_amdgcn_readlane(c4.y, j) : 0u,
-                                        NRP > 8 ? __builtin_amdgcn_readlane(c4.z, j) : 0u,
-                                        NRP > 8 ? __builtin_amdgcn_readlane(c4.w, j) : 0u);
-            if constexpr (kAsm) {
-              u32x8 m = plane_masks_issue(coef_byte(cf, 0));
-#pragma unroll
-              for (int a = 0; a < NQ; ++a) {
-                if constexpr (VEC == 2) {
-                  auto& Za = reinterpret_cast<uint32_t(&)[8][2]>(Z[a]);
-                  if (a + 1 < NQ) m = planes_fold2_next(Za, x[u].v[0], x[u].v[1], m, coef_byte(cf, a + 1));
-                  else planes_fold2(Za, x[u].v[0], x[u].v[1], m);
-                } else {
-                  auto& Za = reinterpret_cast<uint32_t(&)[8][1]>(Z[a]);
-                  if (a + 1 < NQ) m = planes_fold1_next(Za, x[u].v[0], m, coef_byte(cf, a + 1));
-                  else planes_fold1(Za, x[u].v[0], m);
-                }
-              }
-            } else {
-#pragma unroll
-              for (int a = 0; a < NQ; ++a) {
-                const uint32_t ca = coef_byte(cf, a);
-                if constexpr (kBranch) {
-#pragma unroll
-                  for (int kk = 0; kk < 8; ++kk)
-                    if (ca & (1u << kk)) {
-#pragma unroll
-                      for (int v = 0; v < VEC; ++v) Z[a][kk][v] ^= x[u].v[v];
-                    }
-                } else {
-#pragma unroll
-                  for (int kk = 0; kk < 8; ++kk) {
-                    const uint32_t m = 0u - ((ca >> kk) & 1u);
-#pragma unroll
-                    for (int v = 0; v < VEC; ++v) Z[a][kk][v] = mxor(Z[a][kk][v], x[u].v[v], m);
-                  }
-                }
-              }
-            }
-          }
+          if (j < nb) fold_j(x[u], c4, j);  // wave-uniform
           load_row(rb + j + U, x[u]);
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -3244,14 +3377,22 @@ static hipError_t scan_nq(const ScanShape& sh, const uint8_t* d_shard, uint64_t 
                        nrec, sh.pitch, sh.cpr, d_c, d_slabs, acc);
   else
     hipLaunchKernelGGL((k_scan<NQ, NRP, VEC, false>), sh.grid, dim3(kScanThreads), 0, s, d_shard,
-                       nrec, sh.pitch, sh.cpr, d_c, d_slabs, acc);
+                       nrec, sh.pitch, sh.cpr, d_c, d_slabs, acc & 1);
   return hipGetLastError();
 }
 
 hipError_t launch_scan(const ScanShape& sh, const uint8_t* d_shard, uint64_t nrec,
                        const uint8_t* d_c, uint8_t* d_slabs, bool accumulate, hipStream_t s) {
-  const int acc = accumulate ? 1 : 0;
-  if (sh.tfold) return launch_scan_t(sh, d_shard, nrec, d_c, d_slabs, acc, s);
+  // bit 1: the waves of a k_scan_uni / k_scan_t workgroup claim row chunks instead of folding a
+  // fixed range each (round 6: Hollanti 5 rounds 3.60 -> 3.12-3.30 ms, 3 rounds -1.5 %,
+  // profiles/r06/r6w_*, r6x_*; $PIR_SCAN_DYN=0 restores the fixed ranges)
+  const char* dv = getenv("PIR_SCAN_DYN");
+  const int acc = (accumulate ? 1 : 0) | ((dv ? atoi(dv) != 0 : true) ? 2 : 0);
+  if (sh.tfold) {
+    // k_scan_t addresses a workgroup's rows through one buffer resource when they claim chunks
+    const bool wg_fits = (nrec / sh.grid.x + 1) * (uint64_t)sh.pitch < (1ull << 31);
+    return launch_scan_t(sh, d_shard, nrec, d_c, d_slabs, wg_fits ? acc : (acc & 1), s);
+  }
   switch (sh.nq) {
     case 1: return scan_nq<1>(sh, d_shard, nrec, d_c, d_slabs, acc, s);
     case 2: return scan_nq<2>(sh, d_shard, nrec, d_c, d_slabs, acc, s);

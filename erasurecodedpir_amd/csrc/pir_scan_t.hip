@@ -45,7 +45,13 @@ void k_scan_t(const uint8_t* __restrict__ shard, uint64_t nrec, uint32_t pitch, 
   // per wave: T[v] at [v * WD]; read as uint2 (ds_read_b64) when WD == 2, hence 8-aligned
   __shared__ alignas(8) uint32_t tab[kScanTWaves][256 * WD];
   __shared__ uint32_t red[NQ * GW];
+  __shared__ uint32_t next_chunk;
   for (int i = threadIdx.x; i < NQ * GW; i += blockDim.x) red[i] = 0;
+  // accumulate bit 1 (launch_scan_t, $PIR_SCAN_DYN): the waves claim 64-row chunks of the
+  // workgroup's rows (as k_scan_uni: equal-priority waves issue oldest first, so fixed ranges
+  // leave the youngest waves folding the tail alone)
+  const bool dyn = (accumulate >> 1) & 1;
+  accumulate &= 1;
 
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -53,8 +59,14 @@ void k_scan_t(const uint8_t* __restrict__ shard, uint64_t nrec, uint32_t pitch, 
   const uint64_t nwaves = (uint64_t)gridDim.x * kScanTWaves;
   const uint32_t chunk = blockIdx.y * kColGroupLanes + lane;
   const bool active = chunk < cpr;
-  const uint64_t r0 = wave * nrec / nwaves, r1 = (wave + 1) * nrec / nwaves;
+  // the wave's rows, or (dyn) the workgroup's
+  const uint64_t r0 = dyn ? (uint64_t)blockIdx.x * kScanTWaves * nrec / nwaves : wave * nrec / nwaves;
+  const uint64_t r1 = dyn ? ((uint64_t)blockIdx.x + 1) * kScanTWaves * nrec / nwaves : (wave + 1) * nrec / nwaves;
   uint32_t* const tw = &tab[wv][0];
+  if (dyn) {
+    if (threadIdx.x == 0) next_chunk = 0;
+    __syncthreads();
+  }
 
   uint32_t Zt[32][WD];
 #pragma unroll
@@ -101,12 +113,28 @@ void k_scan_t(const uint8_t* __restrict__ shard, uint64_t nrec, uint32_t pitch, 
 #pragma unroll
     for (int r = 0; r < 6; ++r) lm[r] = ((lane >> r) & 1u) ? 0xffffffffu : 0u;
 
+    // chunk claims (dyn): rb walks the claimed chunks' first rows; the rows and coefficient words
+    // loaded ahead come from the next claimed chunk past the current one's end
+    const uint32_t nch = (nrows + 63) / 64;
+    auto claim = [&]() __attribute__((always_inline)) -> uint32_t {
+      uint32_t v = 0;
+      if (lane == 0)
+        v = __hip_atomic_fetch_add(&next_chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return (uint32_t)__builtin_amdgcn_readfirstlane(v);
+    };
+    uint32_t cur = dyn ? claim() : 0u;
+    uint32_t nxt = dyn ? (cur < nch ? claim() : nch) : 1u;
+    // row k >= 0 of the sequence that continues past the current chunk into the next
+    auto seq_row = [&](uint32_t k) __attribute__((always_inline)) -> uint32_t {
+      return k < 64 ? cur * 64 + k : (nxt < nch ? nxt * 64 + (k - 64) : nrows);
+    };
     uint32_t x[16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) x[u] = load_rel((uint32_t)u);
-    uint2 cw = coefs64(0);
-    for (uint32_t rb = 0; rb < nrows; rb += 64) {
-      const uint2 cwn = coefs64(rb + 64);  // the next 64 rows' coefficient words, in flight
+    for (int u = 0; u < 16; ++u) x[u] = load_rel(seq_row((uint32_t)u));
+    uint2 cw = cur < nch ? coefs64(cur * 64) : make_uint2(0, 0);
+    for (; cur < nch;) {
+      const uint32_t rb = cur * 64;
+      const uint2 cwn = nxt < nch ? coefs64(nxt * 64) : make_uint2(0, 0);  // next chunk's words, in flight
       const uint32_t nb = nrows - rb < 64 ? nrows - rb : 64;
       for (uint32_t j0 = 0; j0 < nb; j0 += 16) {
 #pragma unroll
@@ -167,11 +195,13 @@ void k_scan_t(const uint8_t* __restrict__ shard, uint64_t nrec, uint32_t pitch, 
           fold(tb, 3);
           __builtin_amdgcn_wave_barrier();  // reads done before the next group's table
 #pragma unroll
-          for (int r = 0; r < 8; ++r) x[8 * g + r] = load_rel(rb + j + 16 + r);
+          for (int r = 0; r < 8; ++r) x[8 * g + r] = load_rel(seq_row(j + 16 + r));
           __builtin_amdgcn_sched_barrier(0);  // one group at a time (register pressure)
         }
       }
       cw = cwn;
+      cur = nxt;
+      nxt = dyn ? (cur < nch ? claim() : nch) : cur + 1;
     }
   }
   __syncthreads();  // red[] zeroed
