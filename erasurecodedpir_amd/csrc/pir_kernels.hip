@@ -766,6 +766,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
 //             per-bit s_bfe masks held the 8-round batched scan to 1.5 TB/s on the scalar unit).
 // Wave w folds rows [w * nrec / nwaves, (w + 1) * nrec / nwaves) of its column group.
 constexpr uint32_t kScanDynRows = 32;  // k_scan_uni's claimed chunks (four Russians, dyn)
+#ifndef PIR_SCAN_DYN_G
+#define PIR_SCAN_DYN_G 2  // groups of 4 rows in flight per wave in the four-Russians chunk loop
+#endif
 template <int NQ, int NRP, int VEC, int NT = kScanThreads>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kScanThreads ? kScanThreads / 64 * kScanBlocksPerCU / 4 : NT / 256)))
 void k_scan_uni(const uint8_t* __restrict__ shard,
@@ -774,7 +777,10 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
                                                            uint8_t* __restrict__ slabs, int accumulate) {
   constexpr int CH = VEC * 4;
   constexpr int GW = kColGroupLanes * VEC;
-  constexpr int U = NQ <= 2 ? 8 : 4;  // divides 64 (the coefficient block)
+#ifndef PIR_SCAN_U3
+#define PIR_SCAN_U3 4  // rows in flight per lane for 3 rounds at <= 2 dwords per lane
+#endif
+  constexpr int U = NQ <= 2 ? 8 : (NQ == 3 && VEC <= 2 ? PIR_SCAN_U3 : 4);  // divides 64
   constexpr bool kBranch = VEC == 4 || NQ <= 2;
   // four Russians over groups of 4 rows (pir_m4r.h): one dword per lane for 4-8 rounds (8 NQ +
   // 16 VGPRs of planes and row combinations fit the 128 of 16 waves per CU), two dwords for 4-5
@@ -914,7 +920,7 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
       // run ahead across chunk boundaries); every wave's planes are XORed into red[] at the
       // end, so which wave folds a chunk does not matter.  Rows past the workgroup's last take
       // coefficient 0 and re-read its first row.
-      constexpr uint32_t C = kScanDynRows;
+      constexpr uint32_t C = kScanDynRows % (4 * PIR_SCAN_DYN_G) == 0 ? kScanDynRows : 16 * PIR_SCAN_DYN_G;
       if (threadIdx.x == 0) next_chunk = 0;
       __syncthreads();
       const uint64_t wg0 = (uint64_t)blockIdx.x * waves_per_block;
@@ -935,35 +941,48 @@ void k_scan_uni(const uint8_t* __restrict__ shard,
       uint32_t cur = claim();
       if (cur < nch) {
         uint32_t nxt = claim();
-        Chunk<VEC> x[4];
-        uint64_t w[4];
-        bool wv[4];
+        // G groups of 4 rows in flight (rows and coefficient words loaded G groups ahead)
+        constexpr int G = PIR_SCAN_DYN_G;
+        static_assert(C % (4 * G) == 0, "whole group batches per chunk");
+        // row k of the sequence that runs on from the current chunk into the next: its offset
+        // in the workgroup's rows (0 and false past the last row)
+        auto pos = [&](uint32_t k, uint32_t& o) __attribute__((always_inline)) -> bool {
+          const uint32_t nc = k < C ? cur : nxt;
+          o = nc * C + (k < C ? k : k - C);
+          const bool v = nc < nch && o < nrows;
+          if (!v) o = 0u;
+          return v;
+        };
+        Chunk<VEC> x[4 * G];
+        uint64_t w[4 * G];
+        bool wv[4 * G];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t o = cur * C + (uint32_t)r;
-          wv[r] = o < nrows;
-          w[r] = (uint64_t)cwb[wv[r] ? o : 0u];
-          x[r] = load_chunk<VEC>(base + (uint64_t)(wv[r] ? o : 0u) * pitch);
+        for (int q = 0; q < 4 * G; ++q) {
+          uint32_t o;
+          wv[q] = pos((uint32_t)q, o);
+          w[q] = (uint64_t)cwb[o];
+          x[q] = load_chunk<VEC>(base + (uint64_t)o * pitch);
         }
         while (true) {
-          for (uint32_t i = 0; i < C; i += 4) {
-            const uint32_t vi = m4r_index(rfl64(wv[0] ? w[0] : 0), rfl64(wv[1] ? w[1] : 0),
-                                          rfl64(wv[2] ? w[2] : 0), rfl64(wv[3] ? w[3] : 0));
-            __builtin_amdgcn_sched_barrier(0);
-            // the next group: this chunk's, or the first of the next chunk
-            const uint32_t nc = i + 4 < C ? cur : nxt, ni = i + 4 < C ? i + 4 : 0u;
-            uint32_t o[4];
+          for (uint32_t i = 0; i < C; i += 4 * G) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              o[r] = nc * C + ni + (uint32_t)r;
-              wv[r] = nc < nch && o[r] < nrows;
-              if (!wv[r]) o[r] = 0u;
-              w[r] = (uint64_t)cwb[o[r]];
+            for (int g = 0; g < G; ++g) {
+              const int q0 = 4 * g;
+              const uint32_t vi = m4r_index(rfl64(wv[q0] ? w[q0] : 0), rfl64(wv[q0 + 1] ? w[q0 + 1] : 0),
+                                            rfl64(wv[q0 + 2] ? w[q0 + 2] : 0), rfl64(wv[q0 + 3] ? w[q0 + 3] : 0));
+              __builtin_amdgcn_sched_barrier(0);
+              uint32_t o[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                wv[q0 + r] = pos(i + 4u * G + (uint32_t)(q0 + r), o[r]);
+                w[q0 + r] = (uint64_t)cwb[o[r]];
+              }
+              m4r_fold_group<VEC, NQ>(Z, x[q0].v, x[q0 + 1].v, x[q0 + 2].v, x[q0 + 3].v, vi,
+                                      (lane & 7u) * 4u);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) x[q0 + r] = load_chunk<VEC>(base + (uint64_t)o[r] * pitch);
+              __builtin_amdgcn_sched_barrier(0);
             }
-            m4r_fold_group<VEC, NQ>(Z, x[0].v, x[1].v, x[2].v, x[3].v, vi, (lane & 7u) * 4u);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) x[r] = load_chunk<VEC>(base + (uint64_t)o[r] * pitch);
-            __builtin_amdgcn_sched_barrier(0);
           }
           cur = nxt;
           if (cur >= nch) break;
