@@ -1335,9 +1335,9 @@ def run_mp(args, ctx, config):
         ans_dev = lambda dk, dr: eng.answer_mp_dev(dk, p, t, dr)  # noqa: E731
         ans = lambda k: eng.answer_mp(k, p, t)  # noqa: E731
     # the engine's default (answer_mp_locked): k_query's sqrt(N) mode for >= 3 shares or <= 8
-    # seeds a row
+    # seeds a row, at most 32 seeds a row (64 when forced)
     fv = os.environ.get("PIR_MP_FUSED", "1")
-    fused = fv == "2" or (fv != "0" and (nrk >= 3 or p2 <= 8))
+    fused = (fv == "2" and p2 <= 64) or (fv not in ("0", "2") and p2 <= 32 and (nrk >= 3 or p2 <= 8))
     eng = pir.Engine(2, 1, n, efs, nrk, device=ctx.local)
     eng.fill_shard_random(SHARD_SEED)
     d_k = eng.alloc_dev(nkeys * eb)

@@ -852,7 +852,11 @@ int answer_mp_locked(pir_engine* e, const pir::MpLayout& L, const uint8_t* d_key
   if (fmode != 0) {
     const pir::QueryPlan qp = pir::make_query_plan(c.log_num_records, c.log_num_partitions, 2,
                                                    c.num_rounds, e->pitch, e->num_cus);
-    const bool takes = thread_num == 0 && num_threads == 1 && L.nu && L.p2 <= 64 &&
+    // more than 32 seeds per row (CD732: 64): the 4 share waves beside the scan fall behind and
+    // the separate share kernel + scan is faster (3.77 -> 3.56 ms; CD842's 32 seeds and the
+    // multiparty shapes stay fused: 2.82 / 2.51 / 2.64 against 3.15 / 2.66 / 2.81,
+    // profiles/r06/r7i_ccd7_fused_ab.*, r7j_mp_fused_ab.*); $PIR_MP_FUSED=2 forces up to 64
+    const bool takes = thread_num == 0 && num_threads == 1 && L.nu && L.p2 <= (fmode == 2 ? 64u : 32u) &&
                        e->allow_query && qp.tile && qp.shape.uniform &&
                        L.mu % (uint64_t)qp.tile == 0 &&
                        (fmode == 2 || L.nrk >= 3 || L.p2 <= 8);
